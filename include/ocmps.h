@@ -1,0 +1,124 @@
+/*
+ * ocmps.h — C-ABI of the MI355X-native gradient/Hessian inner loop of
+ * fskovbo/OptimalControlMPS (BH_tDMRG time-stepper + OptimalControl
+ * contractions), implemented by liboptimalcontrolmps_amd.so.
+ *
+ * Plain pointers and sizes only; no exceptions cross this boundary.  Every
+ * function returns 0 on success or a nonzero OCG_E* code, with a message in
+ * ocg_last_error(ctx).  The C++ facade (optimalcontrolmps/OptimalControl.hpp)
+ * rethrows as std::runtime_error.  Reference citations are path:line in the
+ * reference repository.
+ *
+ * MPS interchange format ("compact U(1) blocks", the IQMPS replacement):
+ *   dims : int[(L+1)*(Q+1)]   dims[b*(Q+1)+q] = # states of bond b (between
+ *          sites b and b+1; bond 0 and bond L are trivial) whose left particle
+ *          count is q.  Q = number of bosons.
+ *   data : double[2*nelem]    complex, interleaved (re, im); for site
+ *          k = 1..L, sector q = 0..Q, occupation n = 0..p-1 with q+n <= Q and
+ *          both dims nonzero: the block A_k[(q,n)] of dims[k-1][q] x
+ *          dims[k][q+n] entries, row-major.
+ * Every MPS handed in must be right-orthonormal with its orthogonality centre
+ * at site 1 (the form BH_tDMRG::step leaves, src/BH_tDMRG.cpp:217-228).
+ */
+#ifndef OCMPS_H
+#define OCMPS_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCG_OK 0
+#define OCG_EINVAL 1    /* bad argument / shape */
+#define OCG_ECAP 2      /* caller buffer too small, or problem exceeds engine capacity */
+#define OCG_EHIP 3      /* HIP runtime error (no GPU, launch failure, ...) */
+#define OCG_ESTATE 4    /* call order violated (e.g. rows before trajectories) */
+#define OCG_ENUM 5      /* numerical failure flagged by a kernel */
+
+typedef struct ocg_ctx ocg_ctx;
+
+/* Engine limits and per-context sizes (for callers sizing buffers). */
+typedef struct ocg_info {
+  int L, p, Q;
+  size_t mps_max_nelem;   /* complex elements of the largest MPS this context can hold */
+  int lds_bytes;          /* dynamic LDS of one chain workgroup */
+  int block_threads;      /* threads per chain workgroup */
+  int device;
+} ocg_info;
+
+/* --------------------------------------------------------------- context
+ * Replaces BH_tDMRG(sites, J, tstep, {"Cutoff=",cutoff,"Maxm=",maxm})
+ * (reference include/BH_tDMRG.hpp:34, src/BH_tDMRG.cpp:3-15): Bose-Hubbard
+ * chain of L sites, local dimension p (= BoseHubbard d + 1), npart bosons,
+ * hopping J, Trotter step tstep.  maxm <= 0 means ITensor's default (5000).
+ * Builds the forward/backward hopping gates (initJGates, :18-58) and the
+ * dH = sum_k 0.5 n_k(n_k-1) MPO data (:10-14) on `device`. */
+int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm,
+               ocg_ctx** out);
+int ocg_destroy(ocg_ctx* ctx);
+/* last error message of ctx (or of the last failed ocg_create when ctx == NULL) */
+const char* ocg_last_error(const ocg_ctx* ctx);
+int ocg_get_info(const ocg_ctx* ctx, ocg_info* info);
+/* BH_tDMRG::setTstep (src/BH_tDMRG.cpp:61-65) */
+int ocg_set_tstep(ocg_ctx* ctx, double tstep);
+/* number of complex elements of an MPS with the given dims */
+size_t ocg_mps_nelem(int L, int p, int Q, const int* dims);
+
+/* ------------------------------------------ TimeStepper-level operations
+ * Host MPS in, host MPS out (compact format above).  out_cap is the capacity
+ * of out_data in complex elements; *out_nelem receives the size written. */
+
+/* BH_tDMRG::step(psi, from, to, propagateForward) (src/BH_tDMRG.cpp:111-230) */
+int ocg_step(ocg_ctx* ctx, const int* dims, const double* data, double from, double to, int forward,
+             int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem);
+/* nsteps consecutive steps with controls u[0..nsteps] (step i: u[i] -> u[i+1]) */
+int ocg_steps(ocg_ctx* ctx, const int* dims, const double* data, const double* u, int nsteps, int forward,
+              int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem);
+/* overlapC(x, y) = <x|y> (with_dH = 0) or overlapC(x, propDeriv, y) = <x|dH|y>
+ * (with_dH = 1) (src/OptimalControl.cpp:242, :412); out = {re, im} */
+int ocg_overlap(ocg_ctx* ctx, const int* dims_x, const double* x, const int* dims_y, const double* y,
+                int with_dH, double* out);
+/* exactApplyMPO(propDeriv, psi, args) (src/OptimalControl.cpp:256); *norm = ||result|| */
+int ocg_apply_dH(ocg_ctx* ctx, const int* dims, const double* data, int* out_dims, double* out_data,
+                 size_t out_cap, size_t* out_nelem, double* norm);
+
+/* ----------------------------------------- OptimalControl hot path
+ * Device-resident trajectories for one control vector u[0..N-1].
+ * OptimalControl ctor copies of psi_target / psi_init (src/OptimalControl.cpp:10-34). */
+int ocg_set_states(ocg_ctx* ctx, const int* dims_target, const double* target, const int* dims_init,
+                   const double* init);
+/* calcPsi (which & 1, src/OptimalControl.cpp:375-390) and calcXi (which & 2,
+ * :392-407); both chains run concurrently when which == 3 (calcPsiXiDivT's
+ * two threads, :421-438). */
+int ocg_propagate(ocg_ctx* ctx, const double* u, int N, int which);
+/* overlapFactor = overlapC(psi_t[N-1], psi_target) (src/OptimalControl.cpp:242) */
+int ocg_overlap_factor(ocg_ctx* ctx, double* F);
+/* fid[i] = |<psi_target|psi_t[i]>|^2 (calcFidelityForAllT, :548-569) */
+int ocg_fidelities(ocg_ctx* ctx, double* fid);
+/* divT[i] = overlapC(xi_t[i], propDeriv, psi_t[i]) (calcDivT, :409-419); 2N doubles */
+int ocg_div_t(ocg_ctx* ctx, double* divT);
+/* xiHlist[i] = exactApplyMPO(propDeriv, xi_t[i], args) for all i (:300-303) */
+int ocg_xi_dH(ocg_ctx* ctx);
+/* calcHessianRow (:251-279) for rows[0..nrows-1] (each in 1..N-2), F and divT
+ * as produced above (F: 2 doubles, divT: 2N doubles).  Writes the fidelity
+ * Hessian entries (i, j>=i) and their mirrors into H (row-major N x N,
+ * caller-zeroed; entries of different rows are disjoint); the regularisation
+ * Hessian is the caller's.  Requires ocg_propagate(..,3) + ocg_xi_dH. */
+int ocg_hessian_rows(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows, const double* F,
+                     const double* divT, double* H);
+/* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host */
+int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
+
+/* ------------------------------------------------------ instrumentation
+ * Per-kernel HIP-event timing on the context's stream and the algorithmic
+ * traffic model of DESIGN.md §Roofline.  kind: 0 trajectory, 1 overlaps,
+ * 2 dH apply, 3 Hessian rows, 4 steps.  Sums since the last reset. */
+int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
+                     double* alg_flops, long* sweep_steps);
+int ocg_reset_stats(ocg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCMPS_H */

@@ -1,0 +1,44 @@
+// Shared host/device definitions of the MI355X tDMRG chain engine.
+//
+// One workgroup owns one MPS "chain" (a psi_t / xi_t trajectory, or one
+// Hessian row's re-propagated psiH) resident in LDS for its whole life;
+// every Trotter sweep, U(1)-block eigen-decomposition, truncation, gauge move,
+// dH compression and overlap of that chain runs inside the workgroup.
+// See DESIGN.md §Engine for the data layout and roofline.
+#pragma once
+
+#include <stdint.h>
+
+#define OCG_MAXL 48      // sites
+#define OCG_MAXQ1 64     // particle-number sectors (Q+1)
+#define OCG_MAXP 12      // local dimension p = d+1
+#define OCG_MAXGATES 48
+#define OCG_MAXD (2 * OCG_MAXP)
+
+// Kernel parameter block (passed by value).  All capacities are in complex
+// (16-byte) elements unless noted.
+struct OcgParams {
+  int L, p, Q, Q1;          // sites, local dim, particle number, Q+1
+  int nsq;                  // (L+1)*Q1 ints of bond-sector dims per slot
+  int cap;                  // complex elements per MPS slot
+  int site_base[OCG_MAXL + 1];  // [k] base of site k's region (k = 1..L)
+  int site_cap[OCG_MAXL + 1];   // [k] capacity of site k's region
+  int max_site_cap;
+  int thcap;                // two-site / matricisation scratch capacity
+  int ecap;                 // overlap environment capacity (per environment)
+  int evcap;                // eigen-pair list capacity
+  int nrot;                 // rotation-table capacity (pairs)
+  double dt, cutoff;
+  int maxm;
+  double dH[OCG_MAXP];      // 0.5 n (n-1)
+  int ngates;
+  int gate_i1[OCG_MAXGATES];
+  int glo[OCG_MAXD], gsz[OCG_MAXD], goff[OCG_MAXD];  // per-Δ gate blocks
+  int gtotal;               // complex entries of one direction's gate table
+  int lds_bytes;            // dynamic LDS of one chain workgroup
+};
+
+// Truncation used for gauge moves and the left-to-right half of the dH
+// compression (ITensor MPS::position / orthogonalize; parity unpinned, the
+// oracle uses the same value: oracle/tdmrg_oracle.hpp kGaugeCutoff).
+#define OCG_GAUGE_CUTOFF 1e-14

@@ -1,0 +1,636 @@
+// liboptimalcontrolmps_amd: HIP kernels (gfx950) + the C-ABI of include/ocmps.h.
+//
+// Kernels (one workgroup = one MPS chain resident in LDS, engine_device.hpp):
+//   k_trajectory  : psi_t forward chain and xi_t backward chain (calcPsi / calcXi)
+//   k_overlaps    : batched <x|y> / <x|dH|y> (calcDivT, fidelities, overlapFactor)
+//   k_apply_dH    : batched exactApplyMPO(propDeriv, .) (xiHlist)
+//   k_hessian_rows: calcHessianRow — dH psi_i, then re-propagate + overlap per j
+//   k_steps       : TimeStepper::step on host-provided states
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ocmps.h"
+#include "engine.hpp"
+#include "engine_device.hpp"
+#include "params.hpp"
+
+using ocg::Chain;
+
+#ifndef OCG_NT
+#define OCG_NT 64
+#endif
+static constexpr int NT = OCG_NT;
+
+#include "kernels.hpp"
+using ocg::Pool;
+
+// --------------------------------------------------------------------------
+// __global__ entry points
+__global__ __launch_bounds__(NT) void k_trajectory(OcgParams P, const double2* gf, const double2* gb, const int* md,
+                                                   Pool pool, int slot_init, int slot_target, int psi_base,
+                                                   int xi_base, const double* u, int N, int which, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_trajectory<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, u, N, which, stats);
+}
+
+__global__ __launch_bounds__(NT) void k_overlaps(OcgParams P, const double2* gf, const double2* gb, const int* md,
+                                                 Pool pool, const int* xs, const int* ys, int npairs, int with_dH,
+                                                 double2* out, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_overlaps<NT>(smem, P, gf, gb, md, pool, xs, ys, npairs, with_dH, out, stats);
+}
+
+__global__ __launch_bounds__(NT) void k_apply_dH(OcgParams P, const double2* gf, const double2* gb, const int* md,
+                                                 Pool pool, const int* in, const int* outs, int n, double* norms,
+                                                 double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_apply_dH<NT>(smem, P, gf, gb, md, pool, in, outs, n, norms, stats);
+}
+
+__global__ __launch_bounds__(NT) void k_hessian_rows(OcgParams P, const double2* gf, const double2* gb,
+                                                     const int* md, Pool pool, int psi_base, int xih_base,
+                                                     const int* rows, int nrows, const double* u, int N,
+                                                     const double2* divT, double2 F, double* H, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_hessian_rows<NT>(smem, P, gf, gb, md, pool, psi_base, xih_base, rows, nrows, u, N, divT, F, H, stats);
+}
+
+__global__ __launch_bounds__(NT) void k_steps(OcgParams P, const double2* gf, const double2* gb, const int* md,
+                                              Pool pool, const int* slots, int n, const double* u, int u_stride,
+                                              int nsteps, int forward, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_steps<NT>(smem, P, gf, gb, md, pool, slots, n, u, u_stride, nsteps, forward, stats);
+}
+
+// ==========================================================================
+// host side
+// ==========================================================================
+namespace {
+
+thread_local std::string g_create_error;
+
+struct KStat {
+  double ms = 0;
+  long launches = 0;
+};
+
+}  // namespace
+
+struct ocg_ctx {
+  int device = 0;
+  OcgParams P{};
+  double J = 1.0;
+  std::vector<int> md;  // (L+1)*Q1 rank bounds
+  std::string err;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // device buffers
+  double2 *d_gf = nullptr, *d_gb = nullptr;
+  int* d_md = nullptr;
+  Pool pool{nullptr, nullptr};
+  int nslots = 0;
+  double* d_stats = nullptr;  // [5][3]
+  int* d_idx = nullptr;       // index scratch
+  int idx_cap = 0;
+  double* d_u = nullptr;
+  int u_cap = 0;
+  double2* d_c = nullptr;     // complex scratch (overlaps / divT)
+  int c_cap = 0;
+  double* d_H = nullptr;
+  size_t H_cap = 0;
+  double* d_norms = nullptr;
+  // trajectory state
+  int N = 0;
+  bool have_states = false, have_psi = false, have_xi = false, have_xih = false;
+  KStat kst[5];
+  // slot map
+  int slot_init() const { return 0; }
+  int slot_target() const { return 1; }
+  int slot_tmp(int i) const { return 2 + i; }          // 4 scratch slots
+  int psi_base() const { return 6; }
+  int xi_base() const { return 6 + N; }
+  int xih_base() const { return 6 + 2 * N; }
+};
+
+#define HIPCHK(ctx, expr)                                                               \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                   \
+      return OCG_EHIP;                                                                  \
+    }                                                                                   \
+  } while (0)
+
+static int fail(ocg_ctx* c, int code, const std::string& m) {
+  c->err = m;
+  return code;
+}
+
+static int upload_gates(ocg_ctx* c) {
+  std::vector<double> gf, gb;
+  ocg_host::gate_tables(c->P, c->J, gf, gb);
+  const int off = c->P.gtotal;
+  if (!c->d_gf) {
+    HIPCHK(c, hipMalloc(&c->d_gf, sizeof(double2) * off));
+    HIPCHK(c, hipMalloc(&c->d_gb, sizeof(double2) * off));
+  }
+  HIPCHK(c, hipMemcpy(c->d_gf, gf.data(), sizeof(double2) * off, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_gb, gb.data(), sizeof(double2) * off, hipMemcpyHostToDevice));
+  return 0;
+}
+
+static int build_params(ocg_ctx* c, int L, int p, int npart, double tstep, double cutoff, int maxm) {
+  std::string e = ocg_host::build_params(c->P, c->md, L, p, npart, tstep, cutoff, maxm);
+  if (!e.empty()) return fail(c, e.find("too large") != std::string::npos ? OCG_ECAP : OCG_EINVAL, e);
+  return 0;
+}
+
+static int ensure_slots(ocg_ctx* c, int nslots) {
+  if (nslots <= c->nslots) return 0;
+  int n = std::max(nslots, 2 * c->nslots);
+  int* nd = nullptr;
+  double2* nx = nullptr;
+  HIPCHK(c, hipMalloc(&nd, sizeof(int) * size_t(n) * c->P.nsq));
+  HIPCHK(c, hipMalloc(&nx, sizeof(double2) * size_t(n) * c->P.cap));
+  HIPCHK(c, hipMemset(nd, 0, sizeof(int) * size_t(n) * c->P.nsq));
+  if (c->nslots) {
+    HIPCHK(c, hipMemcpy(nd, c->pool.dims, sizeof(int) * size_t(c->nslots) * c->P.nsq, hipMemcpyDeviceToDevice));
+    HIPCHK(c, hipMemcpy(nx, c->pool.data, sizeof(double2) * size_t(c->nslots) * c->P.cap,
+                        hipMemcpyDeviceToDevice));
+    (void)hipFree(c->pool.dims);
+    (void)hipFree(c->pool.data);
+  }
+  c->pool.dims = nd;
+  c->pool.data = nx;
+  c->nslots = n;
+  return 0;
+}
+
+template <class T>
+static int ensure_buf(ocg_ctx* c, T*& ptr, int& cap, int n) {
+  if (n <= cap) return 0;
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  int m = std::max(n, 2 * cap);
+  HIPCHK(c, hipMalloc(&ptr, sizeof(T) * size_t(m)));
+  cap = m;
+  return 0;
+}
+
+// host compact <-> slot layout
+static size_t nelem_of(const OcgParams& P, const int* dims, int k) {
+  size_t s = 0;
+  for (int q = 0; q < P.Q1; ++q)
+    for (int n = 0; n < P.p && q + n <= P.Q; ++n) s += size_t(dims[(k - 1) * P.Q1 + q]) * dims[k * P.Q1 + q + n];
+  return s;
+}
+
+static int validate_dims(ocg_ctx* c, const int* dims) {
+  const OcgParams& P = c->P;
+  if (dims[0] != 1) return fail(c, OCG_EINVAL, "bond 0 must be one state with q = 0");
+  for (int q = 1; q < P.Q1; ++q)
+    if (dims[q] != 0) return fail(c, OCG_EINVAL, "bond 0 must be one state with q = 0");
+  for (int q = 0; q < P.Q1; ++q)
+    if (dims[P.L * P.Q1 + q] != (q == P.Q ? 1 : 0))
+      return fail(c, OCG_EINVAL, "bond L must be one state with q = Q (particle number mismatch?)");
+  for (int b = 0; b <= P.L; ++b)
+    for (int q = 0; q < P.Q1; ++q) {
+      int v = dims[b * P.Q1 + q];
+      if (v < 0) return fail(c, OCG_EINVAL, "negative bond dimension");
+      if (v > c->md[b * P.Q1 + q])
+        return fail(c, OCG_ECAP, "bond " + std::to_string(b) + " sector " + std::to_string(q) +
+                                      " exceeds its Schmidt-rank bound / Maxm");
+    }
+  return 0;
+}
+
+static int upload_mps(ocg_ctx* c, int slot, const int* dims, const double* data) {
+  const OcgParams& P = c->P;
+  if (int rc = validate_dims(c, dims)) return rc;
+  std::vector<double2> buf(P.cap, make_double2(0, 0));
+  size_t off = 0;
+  for (int k = 1; k <= P.L; ++k) {
+    size_t n = nelem_of(P, dims, k);
+    if (n > size_t(P.site_cap[k])) return fail(c, OCG_ECAP, "site tensor exceeds capacity");
+    for (size_t i = 0; i < n; ++i) buf[P.site_base[k] + i] = make_double2(data[2 * (off + i)], data[2 * (off + i) + 1]);
+    off += n;
+  }
+  HIPCHK(c, hipMemcpyAsync(SLOT_D(c->pool, P, slot), dims, sizeof(int) * P.nsq, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(SLOT_X(c->pool, P, slot), buf.data(), sizeof(double2) * P.cap, hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+static int download_mps(ocg_ctx* c, int slot, int* dims, double* data, size_t cap, size_t* nelem) {
+  const OcgParams& P = c->P;
+  std::vector<int> d(P.nsq);
+  std::vector<double2> buf(P.cap);
+  HIPCHK(c, hipMemcpyAsync(d.data(), SLOT_D(c->pool, P, slot), sizeof(int) * P.nsq, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(buf.data(), SLOT_X(c->pool, P, slot), sizeof(double2) * P.cap, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  size_t tot = 0;
+  for (int k = 1; k <= P.L; ++k) tot += nelem_of(P, d.data(), k);
+  if (nelem) *nelem = tot;
+  if (tot > cap) return fail(c, OCG_ECAP, "output buffer too small");
+  std::memcpy(dims, d.data(), sizeof(int) * P.nsq);
+  size_t off = 0;
+  for (int k = 1; k <= P.L; ++k) {
+    size_t n = nelem_of(P, d.data(), k);
+    for (size_t i = 0; i < n; ++i) {
+      data[2 * (off + i)] = buf[P.site_base[k] + i].x;
+      data[2 * (off + i) + 1] = buf[P.site_base[k] + i].y;
+    }
+    off += n;
+  }
+  return 0;
+}
+
+static int begin_kernel(ocg_ctx* c) {
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  return 0;
+}
+static int end_kernel(ocg_ctx* c, int kind) {
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev1));
+  float ms = 0;
+  HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->kst[kind].ms += ms;
+  c->kst[kind].launches += 1;
+  return 0;
+}
+
+static int set_lds(ocg_ctx* c) {
+  const int bytes = c->P.lds_bytes;
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_trajectory, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_overlaps, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_apply_dH, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_hessian_rows, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_steps, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  return 0;
+}
+
+static int finish_params(ocg_ctx* c) {
+  ocg::LdsLayout l = ocg::lds_layout(c->P, NT);
+  c->P.lds_bytes = l.bytes;
+  hipDeviceProp_t prop;
+  HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
+  size_t limit = prop.sharedMemPerBlock;
+  if (prop.maxSharedMemoryPerMultiProcessor > limit) limit = prop.maxSharedMemoryPerMultiProcessor;
+  if (size_t(l.bytes) > limit)
+    return fail(c, OCG_ECAP,
+                "chain workgroup needs " + std::to_string(l.bytes) + " B of LDS (> " + std::to_string(limit) +
+                    "): configuration exceeds the single-workgroup engine (see DESIGN.md §Scope)");
+  return 0;
+}
+
+extern "C" {
+
+const char* ocg_last_error(const ocg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+size_t ocg_mps_nelem(int L, int p, int Q, const int* dims) {
+  size_t s = 0;
+  int Q1 = Q + 1;
+  for (int k = 1; k <= L; ++k)
+    for (int q = 0; q < Q1; ++q)
+      for (int n = 0; n < p && q + n <= Q; ++n) s += size_t(dims[(k - 1) * Q1 + q]) * dims[k * Q1 + q + n];
+  return s;
+}
+
+int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm, ocg_ctx** out) {
+  if (!out) { g_create_error = "out is NULL"; return OCG_EINVAL; }
+  *out = nullptr;
+  auto* c = new ocg_ctx;
+  c->device = device;
+  c->J = J;
+  int rc = build_params(c, L, p, npart, tstep, cutoff, maxm);
+  auto bail = [&](int code) {
+    g_create_error = c->err;
+    ocg_destroy(c);
+    return code;
+  };
+  if (rc) return bail(rc);
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) {
+    c->err = std::string("no HIP device available: ") + hipGetErrorString(e);
+    return bail(OCG_EHIP);
+  }
+  if (device < 0 || device >= ndev) { c->err = "device index out of range"; return bail(OCG_EINVAL); }
+  if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(OCG_EHIP); }
+  if ((rc = finish_params(c))) return bail(rc);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    c->err = "stream/event creation failed";
+    return bail(OCG_EHIP);
+  }
+  if ((rc = upload_gates(c))) return bail(rc);
+  if (hipMalloc(&c->d_md, sizeof(int) * c->md.size()) != hipSuccess ||
+      hipMemcpy(c->d_md, c->md.data(), sizeof(int) * c->md.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMalloc(&c->d_stats, sizeof(double) * 15) != hipSuccess ||
+      hipMemset(c->d_stats, 0, sizeof(double) * 15) != hipSuccess) {
+    c->err = "device allocation failed";
+    return bail(OCG_EHIP);
+  }
+  if ((rc = set_lds(c))) return bail(rc);
+  if ((rc = ensure_slots(c, 8))) return bail(rc);
+  *out = c;
+  return 0;
+}
+
+int ocg_destroy(ocg_ctx* c) {
+  if (!c) return 0;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->d_gf) (void)hipFree(c->d_gf);
+  if (c->d_gb) (void)hipFree(c->d_gb);
+  if (c->d_md) (void)hipFree(c->d_md);
+  if (c->pool.dims) (void)hipFree(c->pool.dims);
+  if (c->pool.data) (void)hipFree(c->pool.data);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->d_idx) (void)hipFree(c->d_idx);
+  if (c->d_u) (void)hipFree(c->d_u);
+  if (c->d_c) (void)hipFree(c->d_c);
+  if (c->d_H) (void)hipFree(c->d_H);
+  if (c->d_norms) (void)hipFree(c->d_norms);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int ocg_get_info(const ocg_ctx* c, ocg_info* info) {
+  if (!c || !info) return OCG_EINVAL;
+  info->L = c->P.L; info->p = c->P.p; info->Q = c->P.Q;
+  info->mps_max_nelem = size_t(c->P.cap);
+  info->lds_bytes = c->P.lds_bytes;
+  info->block_threads = NT;
+  info->device = c->device;
+  return 0;
+}
+
+int ocg_set_tstep(ocg_ctx* c, double tstep) {
+  if (!c) return OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  c->P.dt = tstep;
+  c->have_psi = c->have_xi = c->have_xih = false;
+  return upload_gates(c);
+}
+
+static int launch_steps(ocg_ctx* c, int slot, const double* u, int nsteps, int forward) {
+  const OcgParams& P = c->P;
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, nsteps + 1)) return rc;
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 1)) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * (nsteps + 1), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, &slot, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_steps, dim3(1), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx, 1, c->d_u, nsteps + 1, nsteps, forward, c->d_stats + 4 * 3);
+  return end_kernel(c, 4);
+}
+
+int ocg_steps(ocg_ctx* c, const int* dims, const double* data, const double* u, int nsteps, int forward,
+              int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem) {
+  if (!c || !dims || !data || !u || nsteps < 0) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  int slot = c->slot_tmp(0);
+  if (int rc = upload_mps(c, slot, dims, data)) return rc;
+  if (nsteps > 0)
+    if (int rc = launch_steps(c, slot, u, nsteps, forward)) return rc;
+  return download_mps(c, slot, out_dims, out_data, out_cap, out_nelem);
+}
+
+int ocg_step(ocg_ctx* c, const int* dims, const double* data, double from, double to, int forward, int* out_dims,
+             double* out_data, size_t out_cap, size_t* out_nelem) {
+  double u[2] = {from, to};
+  return ocg_steps(c, dims, data, u, 1, forward, out_dims, out_data, out_cap, out_nelem);
+}
+
+static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::vector<int>& ys, int with_dH,
+                           std::vector<double2>& out) {
+  const OcgParams& P = c->P;
+  int n = int(xs.size());
+  if (n == 0) return 0;
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * n)) return rc;
+  if (int rc = ensure_buf(c, c->d_c, c->c_cap, n)) return rc;
+  std::vector<int> idx(xs);
+  idx.insert(idx.end(), ys.begin(), ys.end());
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_overlaps, dim3(n), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx, c->d_idx + n, n, with_dH, c->d_c, c->d_stats + 1 * 3);
+  if (int rc = end_kernel(c, 1)) return rc;
+  out.resize(n);
+  HIPCHK(c, hipMemcpy(out.data(), c->d_c, sizeof(double2) * n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ocg_overlap(ocg_ctx* c, const int* dims_x, const double* x, const int* dims_y, const double* y, int with_dH,
+                double* out) {
+  if (!c || !dims_x || !x || !dims_y || !y || !out) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = upload_mps(c, c->slot_tmp(0), dims_x, x)) return rc;
+  if (int rc = upload_mps(c, c->slot_tmp(1), dims_y, y)) return rc;
+  std::vector<double2> r;
+  if (int rc = launch_overlaps(c, {c->slot_tmp(0)}, {c->slot_tmp(1)}, with_dH, r)) return rc;
+  out[0] = r[0].x;
+  out[1] = r[0].y;
+  return 0;
+}
+
+static int launch_apply_dH(ocg_ctx* c, const std::vector<int>& in, const std::vector<int>& outs, double* norms) {
+  const OcgParams& P = c->P;
+  int n = int(in.size());
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * n)) return rc;
+  int ncap = 0;
+  if (norms) {
+    if (c->d_norms) (void)hipFree(c->d_norms);
+    c->d_norms = nullptr;
+    if (int rc = ensure_buf(c, c->d_norms, ncap, n)) return rc;
+  }
+  std::vector<int> idx(in);
+  idx.insert(idx.end(), outs.begin(), outs.end());
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_apply_dH, dim3(n), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx, c->d_idx + n, n, norms ? c->d_norms : nullptr, c->d_stats + 2 * 3);
+  if (int rc = end_kernel(c, 2)) return rc;
+  if (norms) HIPCHK(c, hipMemcpy(norms, c->d_norms, sizeof(double) * n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int ocg_apply_dH(ocg_ctx* c, const int* dims, const double* data, int* out_dims, double* out_data, size_t out_cap,
+                 size_t* out_nelem, double* norm) {
+  if (!c || !dims || !data) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = upload_mps(c, c->slot_tmp(0), dims, data)) return rc;
+  double nrm = 0;
+  if (int rc = launch_apply_dH(c, {c->slot_tmp(0)}, {c->slot_tmp(1)}, &nrm)) return rc;
+  if (norm) *norm = nrm;
+  return download_mps(c, c->slot_tmp(1), out_dims, out_data, out_cap, out_nelem);
+}
+
+int ocg_set_states(ocg_ctx* c, const int* dims_target, const double* target, const int* dims_init,
+                   const double* init) {
+  if (!c || !dims_target || !target || !dims_init || !init) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = upload_mps(c, c->slot_target(), dims_target, target)) return rc;
+  if (int rc = upload_mps(c, c->slot_init(), dims_init, init)) return rc;
+  c->have_states = true;
+  c->have_psi = c->have_xi = c->have_xih = false;
+  return 0;
+}
+
+int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
+  if (!c || !u || N < 2 || which < 1 || which > 3) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
+  HIPCHK(c, hipSetDevice(c->device));
+  const OcgParams& P = c->P;
+  if (N != c->N) {
+    c->N = N;
+    c->have_psi = c->have_xi = c->have_xih = false;
+  }
+  if (int rc = ensure_slots(c, 6 + 3 * N)) return rc;
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, N)) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
+  int grid = (which == 3) ? 2 : 1;
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_trajectory, dim3(grid), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+                     c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->d_u, N, which,
+                     c->d_stats + 0 * 3);
+  if (int rc = end_kernel(c, 0)) return rc;
+  if (which & 1) { c->have_psi = true; c->have_xih = c->have_xih && (which & 2); }
+  if (which & 2) { c->have_xi = true; c->have_xih = false; }
+  return 0;
+}
+
+int ocg_overlap_factor(ocg_ctx* c, double* F) {
+  if (!c || !F) return OCG_EINVAL;
+  if (!c->have_psi) return fail(c, OCG_ESTATE, "psi_t not propagated");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<double2> r;
+  // overlapC(psi_t.back(), psi_target) = <psi_T|target>
+  if (int rc = launch_overlaps(c, {c->psi_base() + c->N - 1}, {c->slot_target()}, 0, r)) return rc;
+  F[0] = r[0].x;
+  F[1] = r[0].y;
+  return 0;
+}
+
+int ocg_fidelities(ocg_ctx* c, double* fid) {
+  if (!c || !fid) return OCG_EINVAL;
+  if (!c->have_psi) return fail(c, OCG_ESTATE, "psi_t not propagated");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> xs(c->N, c->slot_target()), ys(c->N);
+  for (int i = 0; i < c->N; ++i) ys[i] = c->psi_base() + i;
+  std::vector<double2> r;
+  if (int rc = launch_overlaps(c, xs, ys, 0, r)) return rc;
+  for (int i = 0; i < c->N; ++i) fid[i] = r[i].x * r[i].x + r[i].y * r[i].y;
+  return 0;
+}
+
+int ocg_div_t(ocg_ctx* c, double* divT) {
+  if (!c || !divT) return OCG_EINVAL;
+  if (!c->have_psi || !c->have_xi) return fail(c, OCG_ESTATE, "psi_t and xi_t must be propagated");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> xs(c->N), ys(c->N);
+  for (int i = 0; i < c->N; ++i) { xs[i] = c->xi_base() + i; ys[i] = c->psi_base() + i; }
+  std::vector<double2> r;
+  if (int rc = launch_overlaps(c, xs, ys, 1, r)) return rc;
+  for (int i = 0; i < c->N; ++i) { divT[2 * i] = r[i].x; divT[2 * i + 1] = r[i].y; }
+  return 0;
+}
+
+int ocg_xi_dH(ocg_ctx* c) {
+  if (!c) return OCG_EINVAL;
+  if (!c->have_xi) return fail(c, OCG_ESTATE, "xi_t not propagated");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int> in(c->N), outs(c->N);
+  for (int i = 0; i < c->N; ++i) { in[i] = c->xi_base() + i; outs[i] = c->xih_base() + i; }
+  if (int rc = launch_apply_dH(c, in, outs, nullptr)) return rc;
+  c->have_xih = true;
+  return 0;
+}
+
+int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, const double* F,
+                     const double* divT, double* H) {
+  if (!c || !u || !rows || !F || !divT || !H || nrows < 0) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (N != c->N || !c->have_psi || !c->have_xih) return fail(c, OCG_ESTATE, "propagate(3) + xi_dH first");
+  for (int r = 0; r < nrows; ++r)
+    if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
+  if (nrows == 0) return 0;
+  HIPCHK(c, hipSetDevice(c->device));
+  const OcgParams& P = c->P;
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, nrows)) return rc;
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, N)) return rc;
+  if (int rc = ensure_buf(c, c->d_c, c->c_cap, N)) return rc;
+  size_t hn = size_t(N) * N;
+  if (hn > c->H_cap) {
+    if (c->d_H) (void)hipFree(c->d_H);
+    HIPCHK(c, hipMalloc(&c->d_H, sizeof(double) * hn));
+    c->H_cap = hn;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, rows, sizeof(int) * nrows, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_c, divT, sizeof(double2) * N, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
+  double2 f2 = make_double2(F[0], F[1]);
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_hessian_rows, dim3(nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+                     c->pool, c->psi_base(), c->xih_base(), c->d_idx, nrows, c->d_u, N, c->d_c, f2, c->d_H,
+                     c->d_stats + 3 * 3);
+  if (int rc = end_kernel(c, 3)) return rc;
+  std::vector<double> h(hn);
+  HIPCHK(c, hipMemcpy(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost));
+  // entries of the requested rows and their mirrors (disjoint per row)
+  for (int r = 0; r < nrows; ++r) {
+    int i = rows[r];
+    for (int j = i; j + 1 < N; ++j) {
+      H[size_t(i) * N + j] = h[size_t(i) * N + j];
+      H[size_t(j) * N + i] = h[size_t(j) * N + i];
+    }
+  }
+  return 0;
+}
+
+int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t cap, size_t* nelem) {
+  if (!c || !dims || !data) return OCG_EINVAL;
+  if (t < 0 || t >= c->N) return fail(c, OCG_EINVAL, "t out of range");
+  bool ok = (which == 0 && c->have_psi) || (which == 1 && c->have_xi) || (which == 2 && c->have_xih);
+  if (!ok) return fail(c, OCG_ESTATE, "requested trajectory not available");
+  HIPCHK(c, hipSetDevice(c->device));
+  int base = which == 0 ? c->psi_base() : (which == 1 ? c->xi_base() : c->xih_base());
+  return download_mps(c, base + t, dims, data, cap, nelem);
+}
+
+int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, double* alg_bytes, double* alg_flops,
+                     long* sweep_steps) {
+  if (!c || kind < 0 || kind > 4) return OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  double s[3];
+  HIPCHK(c, hipMemcpy(s, c->d_stats + 3 * kind, sizeof(s), hipMemcpyDeviceToHost));
+  if (total_ms) *total_ms = c->kst[kind].ms;
+  if (launches) *launches = c->kst[kind].launches;
+  if (alg_bytes) *alg_bytes = s[0];
+  if (alg_flops) *alg_flops = s[1];
+  if (sweep_steps) *sweep_steps = long(s[2] + 0.5);
+  return 0;
+}
+
+int ocg_reset_stats(ocg_ctx* c) {
+  if (!c) return OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemset(c->d_stats, 0, sizeof(double) * 15));
+  for (auto& k : c->kst) k = KStat{};
+  return 0;
+}
+
+}  // extern "C"
