@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Benchmark: Hessian-rows/sec of the gradient/Hessian inner loop on MI355X.
+
+Workload (BASELINE.json configs[1]/[2]): Bose-Hubbard chain
+L=5, Npart=5, d=4 (p=5), maxBondDim=80, cutoff 1e-8, J=1, tstep=0.01, T=2.0
+(N_t=201), GRAPE controls u_i ~ U(2,10) (seed 20261015), psi_init/psi_target
+= ground states at U=2.5/50 (exact diagonalisation; synthetic controls).
+
+One "step" = one full getHessian(u, new_control=true)
+(src/OptimalControl.cpp:341-372): psi_t and xi_t trajectories, divT,
+overlapFactor, xiHlist and all N_t-2 = 199 Hessian rows, plus the gradient
+assembly.  With --gpus N the rows are sharded zig-zag over the ranks (each
+rank recomputes the 400-step precompute) and the N_t x N_t partial Hessians
+are summed onto rank 0 with one RCCL reduce over xGMI.
+
+value = Hessian rows completed per second (whole job).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CFG = dict(L=5, p=5, npart=5, J=1.0, tstep=0.01, T=2.0, maxm=80, cutoff=1e-8, U_init=2.5, U_target=50.0,
+           seed=20261015)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFS = 78.6       # MI355X FP64 vector/matrix spec
+
+
+def zigzag_rows(nrows_total, rank, world):
+    """rows 1..N-2, row i costs N-2-i steps: serpentine assignment balances load"""
+    rows = list(range(1, nrows_total + 1))
+    out = []
+    for blk in range(0, len(rows), world):
+        chunk = rows[blk:blk + world]
+        if (blk // world) % 2 == 1:
+            chunk = chunk[::-1]
+        if rank < len(chunk):
+            out.append(chunk[rank])
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=8)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl")
+    dev = torch.device("cuda", local)
+
+    from optimalcontrolmps_amd import ed
+    from optimalcontrolmps_amd.native import MPS, Engine
+
+    L, p, Q, J, dt = CFG["L"], CFG["p"], CFG["npart"], CFG["J"], CFG["tstep"]
+    Nt = int(round(CFG["T"] / dt)) + 1
+    ini = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, CFG["U_init"])[0], L, p, Q))
+    tgt = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, CFG["U_target"])[0], L, p, Q))
+    u = np.random.default_rng(CFG["seed"]).uniform(2.0, 10.0, Nt)
+    rows = zigzag_rows(Nt - 2, rank, world)
+
+    eng = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
+    eng.set_states(tgt, ini)
+    Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=dev)
+
+    def one_step():
+        eng.propagate(u, 3)                      # calcPsi + calcXi (two chains)
+        divT = eng.div_t()                       # calcDivT
+        F = eng.overlap_factor()                 # overlapFactor
+        g = dt * (divT * F * 1j).real            # calcFidelityGrad (gamma = 0)
+        eng.xi_dH()                              # xiHlist
+        H = eng.hessian_rows(u, rows, F, divT)   # calcHessianRow for this rank's rows
+        if world > 1:
+            Hdev.copy_(torch.from_numpy(H))
+            dist.reduce(Hdev, dst=0)             # RCCL sum of disjoint row entries
+        return g, H
+
+    for _ in range(args.warmup):
+        one_step()
+    eng.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    rows_total = (Nt - 2) * args.steps
+    value = rows_total / elapsed
+    st_rows = eng.stats(3)
+    st_traj = eng.stats(0)
+    row_steps = (Nt - 2) * (Nt - 3) // 2
+    sweep_steps = args.steps * (2 * (Nt - 1) * world + row_steps)
+    result = None
+    if rank == 0:
+        launch_ms = st_rows["ms"] / max(1, st_rows["launches"])
+        bytes_per_launch = st_rows["alg_bytes"] / max(1, st_rows["launches"])
+        flops_per_launch = st_rows["alg_flops"] / max(1, st_rows["launches"])
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+        result = {
+            "metric": "Hessian-rows/sec (getHessian incl. psi/xi/divT/xiH precompute), N=5 d=4 chi=80 T=2.0",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "c128/f64",
+            "data": "synthetic GRAPE controls U(2,10) seed 20261015; ED ground states U=2.5 -> 50",
+            "config": {"workload": "getHessian(u, new_control=true), config 1 (L=5 Npart=5 d=4 maxBondDim=80 "
+                                   "tstep=0.01 T=2.0 GRAPE, N_t=201, 199 rows)",
+                       "rows_per_step": Nt - 2, "parallelism": f"rows sharded zig-zag over {world} GPU(s)"},
+            "sweep_steps_per_sec": sweep_steps / elapsed,
+            "kernels": {
+                "hessian_rows": {"avg_ms": launch_ms, "launches": st_rows["launches"]},
+                "trajectory": {"avg_ms": st_traj["ms"] / max(1, st_traj["launches"])},
+                "overlaps_ms": eng.stats(1)["ms"] / max(1, args.steps),
+                "apply_dH_ms": eng.stats(2)["ms"] / max(1, args.steps),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_hessian_rows",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "alg_bytes_per_launch": bytes_per_launch,
+                "fp64_achieved_tflops": flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0,
+                "fp64_peak_tflops": FP64_PEAK_TFS,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(ini, tgt, u, args.cpu_threads)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ini, tgt, u, threads):
+    """The CPU restatement (oracle/, 'port' — ITensor cannot be built here) timed
+    on host cores: full getHessian with a row worker pool like
+    calcHessian_parallel (src/OptimalControl.cpp:281-338)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    L, p, Q, J, dt = CFG["L"], CFG["p"], CFG["npart"], CFG["J"], CFG["tstep"]
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    st = O.Stepper(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"])
+    oc = O.OC(st, O.MPS(L, p, Q, tgt.dims, tgt.data), O.MPS(L, p, Q, ini.dims, ini.data), len(u), 0.0)
+    reps, total = 0, 0.0
+    while total < 10.0 and reps < 8:
+        total += oc.time_hessian(u, threads)
+        reps += 1
+    Nt = len(u)
+    return {"value": reps * (Nt - 2) / total, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} full getHessian calls (config 1, 199 rows each) on the C++ CPU restatement "
+                      f"(oracle/, not ITensor), {threads} row-worker threads, {total:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

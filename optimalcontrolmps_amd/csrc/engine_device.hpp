@@ -10,7 +10,7 @@
 //
 // Layout of one MPS (HBM slot and LDS copy alike):
 //   dims[b*Q1 + q]  (int)   bond b = 0..L, sector q = left particle count
-//   data            (double2) site k occupies [site_base[k], +site_cap[k]);
+//   data            (zc) site k occupies [site_base[k], +site_cap[k]);
 //                   inside it blocks (q, n) (rows dims[k-1][q], cols
 //                   dims[k][q+n]) are packed row-major in (q, n) order.
 #pragma once
@@ -19,34 +19,64 @@
 
 #include "engine.hpp"
 
+#ifndef OCG_INLINE
+#define OCG_INLINE __attribute__((always_inline))
+#endif
+
 namespace ocg {
 
 // ---------------------------------------------------------------- complex
-__device__ __forceinline__ double2 c2(double x, double y) { return make_double2(x, y); }
-__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return c2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ double2 csub(double2 a, double2 b) { return c2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+// POD complex double (same layout as HIP double2) so it can live behind
+// address-space-3 (LDS) pointers: 32-bit addresses and ds_* instructions.
+struct __attribute__((aligned(16))) zc {
+  double x, y;
+};
+#define LDS __attribute__((address_space(3)))
+__host__ __device__ __forceinline__ zc c2(double x, double y) { zc r; r.x = x; r.y = y; return r; }
+
+// LDS complex buffers: an address-space-3 double* (32-bit addresses, ds_*
+// instructions) with complex element access through a converting reference
+// (clang does not let struct copy/assign operate through AS3 pointers).
+struct lref {
+  LDS double* p;
+  __device__ __forceinline__ operator zc() const { return c2(p[0], p[1]); }
+  __device__ __forceinline__ const lref& operator=(const zc& v) const { p[0] = v.x; p[1] = v.y; return *this; }
+  __device__ __forceinline__ const lref& operator=(const lref& o) const {
+    double a = o.p[0], b = o.p[1];
+    p[0] = a; p[1] = b;
+    return *this;
+  }
+};
+struct lzp {
+  LDS double* p;
+  __device__ __forceinline__ lref operator[](int i) const { return lref{p + 2 * i}; }
+  __device__ __forceinline__ lzp operator+(int i) const { return lzp{p + 2 * i}; }
+  __device__ __forceinline__ bool operator==(const lzp& o) const { return p == o.p; }
+};
+__device__ __forceinline__ zc cadd(zc a, zc b) { return c2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ zc csub(zc a, zc b) { return c2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ zc cmul(zc a, zc b) {
   return c2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
 }
 // conj(a) * b
-__device__ __forceinline__ double2 cjmul(double2 a, double2 b) {
+__device__ __forceinline__ zc cjmul(zc a, zc b) {
   return c2(fma(a.x, b.x, a.y * b.y), fma(a.x, b.y, -a.y * b.x));
 }
-__device__ __forceinline__ double2 cscale(double2 a, double s) { return c2(a.x * s, a.y * s); }
-__device__ __forceinline__ double2 cconj(double2 a) { return c2(a.x, -a.y); }
-__device__ __forceinline__ void cacc(double2& acc, double2 a, double2 b) {  // acc += a*b
+__device__ __forceinline__ zc cscale(zc a, double s) { return c2(a.x * s, a.y * s); }
+__device__ __forceinline__ zc cconj(zc a) { return c2(a.x, -a.y); }
+__device__ __forceinline__ void cacc(zc& acc, zc a, zc b) {  // acc += a*b
   acc.x = fma(a.x, b.x, fma(-a.y, b.y, acc.x));
   acc.y = fma(a.x, b.y, fma(a.y, b.x, acc.y));
 }
-__device__ __forceinline__ void cjacc(double2& acc, double2 a, double2 b) {  // acc += conj(a)*b
+__device__ __forceinline__ void cjacc(zc& acc, zc a, zc b) {  // acc += conj(a)*b
   acc.x = fma(a.x, b.x, fma(a.y, b.y, acc.x));
   acc.y = fma(a.x, b.y, fma(-a.y, b.x, acc.y));
 }
-__device__ __forceinline__ double cabs2(double2 a) { return a.x * a.x + a.y * a.y; }
+__device__ __forceinline__ double cabs2(zc a) { return a.x * a.x + a.y * a.y; }
 
 // ---------------------------------------------------------------- LDS map
 struct LdsLayout {
-  // complex buffers (offsets in double2 units)
+  // complex buffers (offsets in zc units)
   int A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
   int ncplx;
   // double buffers (offsets in doubles, after the complex region)
@@ -127,19 +157,19 @@ template <int NT>
 struct Chain {
   const OcgParams& P;
   int tid;
-  double2 *A, *TH, *G, *G2, *W, *W2, *X, *Y, *CR, *S, *GT, *PH, *ROT;
-  double *LAM, *PP, *RED, *SCAL;
-  int *DIMS, *MD, *BOFF, *BOFFT, *THR, *THC, *THO, *THRO, *THCO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT, *XOFF,
+  lzp A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
+  LDS double *LAM, *PP, *RED, *SCAL;
+  LDS int *DIMS, *MD, *BOFF, *BOFFT, *THR, *THC, *THO, *THRO, *THCO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT, *XOFF,
       *YOFF, *RANK, *KIDX, *PART, *ROLE, *PAIR, *CDIM, *COLD, *COFF, *ISCAL;
 
   __device__ Chain(const OcgParams& P_, char* smem) : P(P_), tid(threadIdx.x) {
     LdsLayout l = lds_layout(P, NT);
-    double2* cb = reinterpret_cast<double2*>(smem);
+    lzp cb{(LDS double*)smem};
     A = cb + l.A; TH = cb + l.TH; G = cb + l.G; G2 = cb + l.G2; W = cb + l.W; W2 = cb + l.W2; X = cb + l.X;
     Y = cb + l.Y; CR = cb + l.CR; S = cb + l.S; GT = cb + l.GT; PH = cb + l.PH; ROT = cb + l.ROT;
-    double* db = reinterpret_cast<double*>(cb + l.ncplx);
+    LDS double* db = (cb + l.ncplx).p;
     LAM = db + l.LAM; PP = db + l.PP; RED = db + l.RED; SCAL = db + l.SCAL;
-    int* ib = reinterpret_cast<int*>(db + l.ndbl);
+    LDS int* ib = (LDS int*)(db + l.ndbl);
     DIMS = ib + l.DIMS; MD = ib + l.MD; BOFF = ib + l.BOFF; BOFFT = ib + l.BOFFT; THR = ib + l.THR; THC = ib + l.THC;
     THO = ib + l.THO; THRO = ib + l.THRO; THCO = ib + l.THCO; NQ = ib + l.NQ; SIDE = ib + l.SIDE;
     GOFF = ib + l.GOFF; EOFF = ib + l.EOFF; MQ = ib + l.MQ; POFF = ib + l.POFF; KEPT = ib + l.KEPT;
@@ -151,11 +181,11 @@ struct Chain {
   __device__ __forceinline__ void sync() { __syncthreads(); }
   __device__ __forceinline__ int d(int b, int q) const { return (q < 0 || q > P.Q) ? 0 : DIMS[b * P.Q1 + q]; }
   __device__ __forceinline__ int bo(int k, int q, int n) const { return BOFF[((k - 1) * P.Q1 + q) * P.p + n]; }
-  __device__ __forceinline__ double2* site(int k) { return A + P.site_base[k]; }
+  __device__ __forceinline__ lzp site(int k) { return A + P.site_base[k]; }
 
   // ------------------------------------------------------------- tables
   // block offsets of site k from the current dims (single thread)
-  __device__ int site_offsets_serial(int k, int* out) const {
+  __device__ OCG_INLINE int site_offsets_serial(int k, LDS int* out) const {
     int off = 0;
     for (int q = 0; q < P.Q1; ++q)
       for (int n = 0; n < P.p; ++n) {
@@ -165,7 +195,7 @@ struct Chain {
       }
     return off;
   }
-  __device__ void all_offsets() {  // parallel over sites
+  __device__ OCG_INLINE void all_offsets() {  // parallel over sites
     for (int k = 1 + tid; k <= P.L; k += NT) site_offsets_serial(k, BOFF + (k - 1) * P.Q1 * P.p);
   }
   // (q, local) of the idx-th state of bond b
@@ -184,7 +214,7 @@ struct Chain {
     return s;
   }
   // segment lookup in a (Q1 x p) offset table: find n with off[n] <= r < off[n] + len(n)
-  __device__ __forceinline__ int seg_find(const int* offs, int r) const {
+  __device__ __forceinline__ int seg_find(const LDS int* offs, int r) const {
     int best = -1, bo = -1;
     for (int n = 0; n < P.p; ++n) {
       int o = offs[n];
@@ -193,21 +223,21 @@ struct Chain {
     return best;
   }
   // flat element -> block q using prefix table off[0..Q1]
-  __device__ __forceinline__ int blk_find(const int* off, int e) const {
+  __device__ __forceinline__ int blk_find(const LDS int* off, int e) const {
     int q = 0;
     while (q + 1 < P.Q1 && off[q + 1] <= e) ++q;
     return q;
   }
 
   // ------------------------------------------------------------- I/O
-  __device__ void load(const int* gdims, const double2* gdata) {
+  __device__ OCG_INLINE void load(const int* gdims, const zc* gdata) {
     for (int i = tid; i < P.nsq; i += NT) DIMS[i] = gdims[i];
     for (int i = tid; i < P.cap; i += NT) A[i] = gdata[i];
     sync();
     all_offsets();
     sync();
   }
-  __device__ void store(int* gdims, double2* gdata) {
+  __device__ OCG_INLINE void store(int* gdims, zc* gdata) {
     for (int i = tid; i < P.nsq; i += NT) gdims[i] = DIMS[i];
     for (int k = 1; k <= P.L; ++k) {
       // number of used elements of site k
@@ -223,13 +253,13 @@ struct Chain {
   // gate tables and the per-sector rank bound md[b][q] (Hilbert-space
   // Schmidt-rank bound, capped by Maxm) used to clamp numerically-zero
   // directions out of every decomposition (guards the LDS capacities).
-  __device__ void load_tables(const double2* gf, const double2* gb, const int* md) {
+  __device__ OCG_INLINE void load_tables(const zc* gf, const zc* gb, const int* md) {
     for (int i = tid; i < P.gtotal; i += NT) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
     for (int i = tid; i < 2 * P.nsq; i += NT) MD[i] = md[i];
   }
 
   // ------------------------------------------------------------- norms
-  __device__ double block_reduce_sum(double v) {
+  __device__ OCG_INLINE double block_reduce_sum(double v) {
     RED[tid] = v;
     sync();
     for (int s = NT / 2; s > 0; s >>= 1) {
@@ -240,7 +270,7 @@ struct Chain {
     sync();
     return r;
   }
-  __device__ double site_norm2(int k) {
+  __device__ OCG_INLINE double site_norm2(int k) {
     int n = P.site_cap[k];
     // sum over used blocks only (unused tail may hold stale data)
     double acc = 0;
@@ -254,18 +284,18 @@ struct Chain {
     (void)n;
     return block_reduce_sum(acc);
   }
-  __device__ void site_scale(int k, double f) {
+  __device__ OCG_INLINE void site_scale(int k, double f) {
     for (int i = tid; i < P.site_cap[k]; i += NT) site(k)[i] = cscale(site(k)[i], f);
     sync();
   }
   // multiply site k by a per-physical-index phase table ph[n]
-  __device__ void site_phase(int k, const double2* ph) {
+  __device__ OCG_INLINE void site_phase(int k, lzp ph) {
     for (int q = 0; q < P.Q1; ++q)
       for (int n = 0; n < P.p; ++n) {
         int o = bo(k, q, n);
         if (o < 0) continue;
         int sz = d(k - 1, q) * d(k, q + n);
-        double2 f = ph[n];
+        zc f = ph[n];
         for (int i = tid; i < sz; i += NT) site(k)[o + i] = cmul(site(k)[o + i], f);
       }
     sync();
@@ -274,7 +304,7 @@ struct Chain {
   // ------------------------------------------------------------- Θ
   // Two-site tensor for bond (i1, i1+1), blocks by middle QN q:
   //   rows (n1, a in bond i1-1 sector q-n1), cols (n2, c in bond i1+1 sector q+n2)
-  __device__ void build_theta(int i1) {
+  __device__ OCG_INLINE void build_theta(int i1) {
     const int l = i1 - 1, mid = i1, r = i1 + 1, p = P.p;
     if (tid == 0) {
       int off = 0;
@@ -306,11 +336,11 @@ struct Chain {
       int n1 = seg_find(THRO + q * p, row), n2 = seg_find(THCO + q * p, col);
       int ia = row - THRO[q * p + n1], ic = col - THCO[q * p + n2];
       int dm = d(mid, q);
-      double2 acc = c2(0, 0);
+      zc acc = c2(0, 0);
       if (dm > 0) {
-        const double2* X1 = site(i1) + bo(i1, q - n1, n1) + ia * dm;
+        lzp X1 = site(i1) + bo(i1, q - n1, n1) + ia * dm;
         int drc = d(r, q + n2);
-        const double2* X2 = site(r) + bo(r, q, n2) + ic;
+        lzp X2 = site(r) + bo(r, q, n2) + ic;
         for (int b = 0; b < dm; ++b) cacc(acc, X1[b], X2[b * drc]);
       }
       TH[e] = acc;
@@ -320,53 +350,46 @@ struct Chain {
 
   // pre-phase -> hopping gate (per Δ = n1+n2 block) -> post-phase, on every
   // (a, c) vector of Θ.  mode 0: left-moving (UF both, optional lonely UT on
-  // n2); mode 1: right-moving (UT both after the gate).
-  __device__ void apply_gate(int i1, int forward, int mode, int lonely) {
-    const int l = i1 - 1, r = i1 + 1, p = P.p;
-    const double2* gt = GT + (forward ? 0 : P.gtotal);
-    const double2* UF = PH;
-    const double2* UT = PH + p;
-    int chl = bond_dim(l), chr = bond_dim(r);
-    int tot = chl * chr;
-    for (int t = tid; t < tot; t += NT) {
-      int ia_g = t / chr, ic_g = t - ia_g * chr;
-      int ql, ia, qr, ic;
-      bond_split(l, ia_g, ql, ia);
-      bond_split(r, ic_g, qr, ic);
-      int D = qr - ql;
-      if (D < 0 || D > 2 * (p - 1)) continue;
-      int lo = P.glo[D], sz = P.gsz[D];
-      double2 v[OCG_MAXP], w[OCG_MAXP];
+  // n2); mode 1: right-moving (UT both after the gate).  One thread per
+  // output element (no runtime-indexed private arrays); the result goes to X
+  // and the TH/X buffers are swapped.
+  __device__ OCG_INLINE void apply_gate(int i1, int forward, int mode, int lonely) {
+    const int p = P.p;
+    lzp gt = GT + (forward ? 0 : P.gtotal);
+    lzp UF = PH;
+    lzp UT = PH + p;
+    const int tot = ISCAL[I_THT];
+    for (int e = tid; e < tot; e += NT) {
+      int q = blk_find(THO, e);
+      int loc = e - THO[q], C = THC[q];
+      int row = loc / C, col = loc - row * C;
+      int a1 = seg_find(THRO + q * p, row), a2 = seg_find(THCO + q * p, col);
+      int ia = row - THRO[q * p + a1], ic = col - THCO[q * p + a2];
+      int D = a1 + a2, ql = q - a1;
+      int lo = P.glo[D], sz = P.gsz[D], y = a1 - lo;
+      lzp g = gt + P.goff[D] + y * sz;
+      zc acc = c2(0, 0);
       for (int x = 0; x < sz; ++x) {
-        int n1 = lo + x, n2 = D - n1, q = ql + n1;
-        double2 z = TH[THO[q] + (THRO[q * p + n1] + ia) * THC[q] + THCO[q * p + n2] + ic];
+        int n1 = lo + x, n2 = D - n1, qs = ql + n1;
+        zc z = TH[THO[qs] + (THRO[qs * p + n1] + ia) * THC[qs] + THCO[qs * p + n2] + ic];
         if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
-        v[x] = z;
+        cacc(acc, g[x], z);
       }
-      const double2* g = gt + P.goff[D];
-      for (int y = 0; y < sz; ++y) {
-        double2 acc = c2(0, 0);
-        for (int x = 0; x < sz; ++x) cacc(acc, g[y * sz + x], v[x]);
-        int a1 = lo + y, a2 = D - a1;
-        if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
-        else if (lonely) acc = cmul(acc, UT[a2]);
-        w[y] = acc;
-      }
-      for (int x = 0; x < sz; ++x) {
-        int n1 = lo + x, n2 = D - n1, q = ql + n1;
-        TH[THO[q] + (THRO[q * p + n1] + ia) * THC[q] + THCO[q * p + n2] + ic] = w[x];
-      }
+      if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
+      else if (lonely) acc = cmul(acc, UT[a2]);
+      X[e] = acc;
     }
     sync();
+    lzp t = TH; TH = X; X = t;
   }
 
   // ------------------------------------------------------------- Jacobi
   // Parallel (round-robin) complex Jacobi on all Gram blocks at once.
   // Block q: n = NQ[q] at G + GOFF[q]; eigenvectors accumulated in W.
   // On exit G/W point at the converged buffers (diag = eigenvalues).
-  __device__ void jacobi(double2*& Gc, double2*& Wc) {
-    double2* Gn = (Gc == G) ? G2 : G;
-    double2* Wn = (Wc == W) ? W2 : W;
+  __device__ OCG_INLINE void jacobi(lzp& Gc, lzp& Wc) {
+    lzp Gn = (Gc == G) ? G2 : G;
+    lzp Wn = (Wc == W) ? W2 : W;
     const int maxr = ISCAL[I_MAXROUNDS];
     if (maxr <= 0) return;
     const int npair = ISCAL[I_NPAIR];
@@ -382,14 +405,14 @@ struct Chain {
           if (k == 0) { pp_ = m - 1; qq_ = rnd; }
           else { pp_ = (rnd + k) % (m - 1); qq_ = (rnd - k + m - 1) % (m - 1); }
           if (pp_ > qq_) { int tmp = pp_; pp_ = qq_; qq_ = tmp; }
-          double2 cs = c2(1.0, 0.0), e = c2(1.0, 0.0);
+          zc cs = c2(1.0, 0.0), e = c2(1.0, 0.0);
           double shift = 0.0;
           bool rot = false;
           if (active && qq_ < n) {
-            const double2* g = Gc + GOFF[q];
-            double2 b = g[pp_ * n + qq_];
+            lzp g = Gc + GOFF[q];
+            zc b = g[pp_ * n + qq_];
             double ab = hypot(b.x, b.y);  // no underflow: e = b/|b| must stay unit-modulus
-            double app = g[pp_ * n + pp_].x, aqq = g[qq_ * n + qq_].x;
+            double app = zc(g[pp_ * n + pp_]).x, aqq = zc(g[qq_ * n + qq_]).x;
             // skip rotations whose off-diagonal is below working precision of the diagonal
             if (ab > 1e-300 && ab > 1e-18 * (fabs(app) + fabs(aqq))) {
               double tau = (aqq - app) / (2.0 * ab);
@@ -430,21 +453,21 @@ struct Chain {
           int loc = e - GOFF[q];
           int i = loc / n, j = loc - i * n;
           int base = EOFF[q];
-          const double2* g = (isW ? Wc : Gc) + GOFF[q];
+          lzp g = (isW ? Wc : Gc) + GOFF[q];
           if (MQ[q] == 0) {  // 1x1 block: nothing to rotate
             (isW ? Wn : Gn)[GOFF[q] + loc] = g[loc];
             continue;
           }
           // column-j coefficients of J: J[j][j], J[j'][j]
           int rj = ROLE[base + j], pj = PART[base + j];
-          double2 jjj, jpj;
+          zc jjj, jpj;
           if (rj == 2) { jjj = c2(1, 0); jpj = c2(0, 0); pj = j; }
           else {
-            double2 cs = ROT[2 * PAIR[base + j]], ee = ROT[2 * PAIR[base + j] + 1];
+            zc cs = ROT[2 * PAIR[base + j]], ee = ROT[2 * PAIR[base + j] + 1];
             if (rj == 0) { jjj = c2(cs.x, 0); jpj = cscale(cconj(ee), -cs.y); }  // J[p][p]=c, J[q][p]=-s e*
             else { jjj = cscale(cconj(ee), cs.x); jpj = c2(cs.y, 0); }          // J[q][q]=c e*, J[p][q]=s
           }
-          double2 out;
+          zc out;
           if (isW) {
             // W'[i][j] = W[i][j] J[j][j] + W[i][j'] J[j'][j]
             out = cmul(g[i * n + j], jjj);
@@ -457,21 +480,21 @@ struct Chain {
               out = c2(0, 0);
             } else if (ri != 2 && i == j) {
               double sh = LAM[base + (ri == 0 ? i : pi)];
-              out = c2(g[i * n + i].x + (ri == 0 ? -sh : sh), 0);
+              out = c2(zc(g[i * n + i]).x + (ri == 0 ? -sh : sh), 0);
             } else {
-              double2 jii, jpi;
+              zc jii, jpi;
               if (ri == 2) { jii = c2(1, 0); jpi = c2(0, 0); pi = i; }
               else {
-                double2 cs = ROT[2 * PAIR[base + i]], ee = ROT[2 * PAIR[base + i] + 1];
+                zc cs = ROT[2 * PAIR[base + i]], ee = ROT[2 * PAIR[base + i] + 1];
                 if (ri == 0) { jii = c2(cs.x, 0); jpi = cscale(cconj(ee), -cs.y); }
                 else { jii = cscale(cconj(ee), cs.x); jpi = c2(cs.y, 0); }
               }
               // sum_{k in {i,i'}} sum_{l in {j,j'}} conj(J[k][i]) G[k][l] J[l][j]
-              double2 r0 = cmul(g[i * n + j], jjj);
+              zc r0 = cmul(g[i * n + j], jjj);
               if (rj != 2) cacc(r0, g[i * n + pj], jpj);
               out = cjmul(jii, r0);
               if (ri != 2) {
-                double2 r1 = cmul(g[pi * n + j], jjj);
+                zc r1 = cmul(g[pi * n + j], jjj);
                 if (rj != 2) cacc(r1, g[pi * n + pj], jpj);
                 cjacc(out, jpi, r1);
               }
@@ -480,8 +503,8 @@ struct Chain {
           }
         }
         sync();
-        double2* tg = Gc; Gc = Gn; Gn = tg;
-        double2* tw = Wc; Wc = Wn; Wn = tw;
+        lzp tg = Gc; Gc = Gn; Gn = tg;
+        lzp tw = Wc; Wc = Wn; Wn = tw;
       }
       // convergence check: per block off-diagonal weight vs diagonal weight
       int fl = (sweep & 1) ? I_FLAG1 : I_FLAG0;
@@ -490,14 +513,14 @@ struct Chain {
       for (int q = tid; q < P.Q1; q += NT) {
         int n = NQ[q];
         if (n < 2) continue;
-        const double2* g = Gc + GOFF[q];
+        lzp g = Gc + GOFF[q];
         double off = 0, dia = 0;
         for (int i = 0; i < n; ++i)
           for (int j = 0; j < n; ++j) {
             double a = cabs2(g[i * n + j]);
             if (i == j) dia += a; else off += a;
           }
-        if (off > 1e-30 * dia) atomicOr(&ISCAL[fl], 1);
+        if (off > 1e-30 * dia) atomicOr((int*)&ISCAL[fl], 1);
       }
       sync();
       int more = ISCAL[fl];
@@ -516,7 +539,7 @@ struct Chain {
   // If `normalize`, the norm-carrying factor is divided by sqrt(kept weight).
   // `bound` = per-sector rank bound of the new bond (MD row, or MDZ row in
   // the dH zip-up); vectors beyond it are numerically zero and dropped.
-  __device__ void decompose(int dir, double cutoff, int maxm, bool normalize, const int* bound) {
+  __device__ OCG_INLINE void decompose(int dir, double cutoff, int maxm, bool normalize, const LDS int* bound) {
     if (tid == 0) {
       int go = 0, eo = 0, po = 0, maxr = 0;
       for (int q = 0; q < P.Q1; ++q) {
@@ -544,9 +567,9 @@ struct Chain {
       int q = blk_find(GOFF, e);
       int n = NQ[q], loc = e - GOFF[q];
       int i = loc / n, j = loc - i * n;
-      const double2* T = TH + THO[q];
+      lzp T = TH + THO[q];
       int R = THR[q], C = THC[q];
-      double2 acc = c2(0, 0);
+      zc acc = c2(0, 0);
       if (SIDE[q] == 0) {
         for (int c = 0; c < C; ++c) cacc(acc, T[i * C + c], cconj(T[j * C + c]));
       } else {
@@ -556,37 +579,15 @@ struct Chain {
       W[e] = (i == j) ? c2(1, 0) : c2(0, 0);
     }
     sync();
-    double2* Gc = G;
-    double2* Wc = W;
-#ifdef OCG_EMU_DEBUG
-    if (tid == 0 && getenv("OCG_DBG_G"))
-      for (int q = 0; q < P.Q1; ++q) {
-        int n = NQ[q];
-        if (n < 2) continue;
-        printf("G0 blk %d:\n", q);
-        for (int i = 0; i < n; ++i) { for (int j = 0; j < n; ++j) printf(" (%.4f,%.4f)", G[GOFF[q] + i * n + j].x, G[GOFF[q] + i * n + j].y); printf("\n"); }
-      }
-    sync();
-#endif
+    lzp Gc = G;
+    lzp Wc = W;
     jacobi(Gc, Wc);
-#ifdef OCG_EMU_DEBUG
-    if (tid == 0 && getenv("OCG_DBG_G"))
-      for (int q = 0; q < P.Q1; ++q) {
-        int n = NQ[q];
-        if (n < 2) continue;
-        printf("G blk %d:\n", q);
-        for (int i = 0; i < n; ++i) { for (int j = 0; j < n; ++j) printf(" (%.4g,%.4g)", Gc[GOFF[q] + i * n + j].x, Gc[GOFF[q] + i * n + j].y); printf("\n"); }
-        printf("W blk %d:\n", q);
-        for (int i = 0; i < n; ++i) { for (int j = 0; j < n; ++j) printf(" (%.4f,%.4f)", Wc[GOFF[q] + i * n + j].x, Wc[GOFF[q] + i * n + j].y); printf("\n"); }
-      }
-    sync();
-#endif
     // eigenvalues + global ranking (descending; ties by flat index)
     const int T = ISCAL[I_EVT];
     for (int e = tid; e < T; e += NT) {
       int q = blk_find(EOFF, e);
       int i = e - EOFF[q], n = NQ[q];
-      double lam = Gc[GOFF[q] + i * n + i].x;
+      double lam = zc(Gc[GOFF[q] + i * n + i]).x;
       LAM[e] = lam > 0 ? lam : 0.0;
     }
     sync();
@@ -646,18 +647,6 @@ struct Chain {
     }
     // kept eigenvector order within each block (by global rank)
     sync();
-#ifdef OCG_EMU_DEBUG
-    if (tid == 0) {
-      printf("decompose dir=%d T=%d m=%d total=%g\n", dir, T, ISCAL[I_M], SCAL[S_TOTAL]);
-      for (int q = 0; q < P.Q1; ++q) {
-        printf("  q=%d R=%d C=%d n=%d side=%d kept=%d md=%d lam:", q, THR[q], THC[q], NQ[q], SIDE[q], KEPT[q],
-               bound[q]);
-        for (int i = 0; i < NQ[q]; ++i) printf(" %.3e(r%d)", LAM[EOFF[q] + i], RANK[EOFF[q] + i]);
-        printf("\n");
-      }
-    }
-    sync();
-#endif
     const int m = ISCAL[I_M];
     for (int e = tid; e < T; e += NT) {
       int rk = RANK[e];
@@ -677,19 +666,19 @@ struct Chain {
       int q = blk_find(isX ? XOFF : YOFF, e);
       int k = KEPT[q], R = THR[q], C = THC[q], n = NQ[q];
       int loc = e - (isX ? XOFF[q] : YOFF[q]);
-      const double2* Tq = TH + THO[q];
-      const double2* Wq = Wc + GOFF[q];
+      lzp Tq = TH + THO[q];
+      lzp Wq = Wc + GOFF[q];
       if (isX) {
         int row = loc / k, j = loc - row * k;
         int w = KIDX[EOFF[q] + j];
         double lam = LAM[EOFF[q] + w];
         double sig = sqrt(lam);
-        double2 out;
+        zc out;
         if (SIDE[q] == 0) {
           out = Wq[row * n + w];                       // u exact
           if (dir == kFromright) out = cscale(out, sig * inv);
         } else {
-          double2 acc = c2(0, 0);                      // Θ w
+          zc acc = c2(0, 0);                      // Θ w
           for (int c = 0; c < C; ++c) cacc(acc, Tq[row * C + c], Wq[c * n + w]);
           if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
@@ -700,12 +689,12 @@ struct Chain {
         int w = KIDX[EOFF[q] + j];
         double lam = LAM[EOFF[q] + w];
         double sig = sqrt(lam);
-        double2 out;
+        zc out;
         if (SIDE[q] == 1) {
           out = cconj(Wq[col * n + w]);                // v^H exact
           if (dir == kFromleft) out = cscale(out, sig * inv);
         } else {
-          double2 acc = c2(0, 0);                      // w^H Θ
+          zc acc = c2(0, 0);                      // w^H Θ
           for (int r = 0; r < R; ++r) cjacc(acc, Wq[r * n + w], Tq[r * C + col]);
           if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
@@ -717,7 +706,7 @@ struct Chain {
   }
 
   // write X (rows (n1,a)) into site i1 and Y (cols (n2,c)) into site i1+1
-  __device__ void scatter_two_site(int i1) {
+  __device__ OCG_INLINE void scatter_two_site(int i1) {
     const int r = i1 + 1, p = P.p;
     if (tid == 0) {
       for (int q = 0; q < P.Q1; ++q) DIMS[i1 * P.Q1 + q] = KEPT[q];
@@ -752,7 +741,7 @@ struct Chain {
   // single-site matricisation of site k into TH
   //   left (Fromleft grouping): rows (n, a in bond k-1 sector q-n), cols c in bond k sector q
   //   right (Fromright grouping): rows a in bond k-1 sector q, cols (n, c in bond k sector q+n)
-  __device__ void site_to_theta(int k, bool left) {
+  __device__ OCG_INLINE void site_to_theta(int k, bool left) {
     const int p = P.p;
     if (tid == 0) {
       int off = 0;
@@ -786,7 +775,7 @@ struct Chain {
       int q = blk_find(THO, e);
       int loc = e - THO[q], C = THC[q];
       int row = loc / C, col = loc - row * C;
-      double2 v;
+      zc v;
       if (left) {
         int n = seg_find(THRO + q * p, row);
         int ia = row - THRO[q * p + n];
@@ -802,7 +791,7 @@ struct Chain {
   }
 
   // move the orthogonality centre k -> k+1 (ITensor position, one bond)
-  __device__ void gauge_right(int k, double cutoff, int maxm) {
+  __device__ OCG_INLINE void gauge_right(int k, double cutoff, int maxm) {
     const int p = P.p;
     site_to_theta(k, true);
     decompose(kFromleft, cutoff, maxm, false, MD + k * P.Q1);
@@ -824,10 +813,10 @@ struct Chain {
         if (o < 0) continue;
         int kq = KEPT[q], cc = d(k + 1, q + n), dold = d(k, q);
         int oo = bo(k + 1, q, n);
-        const double2* Yq = Y + YOFF[q];
+        lzp Yq = Y + YOFF[q];
         for (int e = tid; e < kq * cc; e += NT) {
           int i = e / cc, j = e - i * cc;
-          double2 acc = c2(0, 0);
+          zc acc = c2(0, 0);
           if (oo >= 0)
             for (int b = 0; b < dold; ++b) cacc(acc, Yq[i * dold + b], site(k + 1)[oo + b * cc + j]);
           S[o + e] = acc;
@@ -858,26 +847,10 @@ struct Chain {
       }
     for (int e = tid; e < ns; e += NT) site(k + 1)[e] = S[e];
     sync();
-#ifdef OCG_EMU_DEBUG
-    if (tid == 0) {
-      printf("gauge_right(%d) done: ns=%d\n", k, ns);
-      for (int kk = k; kk <= k + 1; ++kk)
-        for (int q = 0; q < P.Q1; ++q)
-          for (int n = 0; n < P.p; ++n) {
-            int o = bo(kk, q, n);
-            if (o < 0) continue;
-            int sz = d(kk - 1, q) * d(kk, q + n);
-            double a = 0;
-            for (int i = 0; i < sz; ++i) a += cabs2(site(kk)[o + i]);
-            printf("   site %d blk(%d,%d) off=%d %dx%d |.|^2=%.4e\n", kk, q, n, o, d(kk - 1, q), d(kk, q + n), a);
-          }
-    }
-    sync();
-#endif
   }
 
   // move the orthogonality centre k -> k-1
-  __device__ void gauge_left(int k, double cutoff, int maxm) {
+  __device__ OCG_INLINE void gauge_left(int k, double cutoff, int maxm) {
     const int p = P.p;
     site_to_theta(k, false);
     decompose(kFromright, cutoff, maxm, false, MD + (k - 1) * P.Q1);
@@ -898,10 +871,10 @@ struct Chain {
         if (o < 0) continue;
         int q = ql + n, kq = KEPT[q], rr = d(k - 2, ql), dold = d(k - 1, q);
         int oo = bo(k - 1, ql, n);
-        const double2* Xq = X + XOFF[q];
+        lzp Xq = X + XOFF[q];
         for (int e = tid; e < rr * kq; e += NT) {
           int i = e / kq, j = e - i * kq;
-          double2 acc = c2(0, 0);
+          zc acc = c2(0, 0);
           if (oo >= 0)
             for (int b = 0; b < dold; ++b) cacc(acc, site(k - 1)[oo + i * dold + b], Xq[b * kq + j]);
           S[o + e] = acc;
@@ -933,14 +906,18 @@ struct Chain {
     sync();
   }
 
-  __device__ void position(int& centre, int target) {
-    while (centre < target) { gauge_right(centre, OCG_GAUGE_CUTOFF, 1 << 30); ++centre; }
-    while (centre > target) { gauge_left(centre, OCG_GAUGE_CUTOFF, 1 << 30); --centre; }
+  __device__ OCG_INLINE void position(int& centre, int target) {
+    while (centre != target) {
+      if (centre < target) { gauge_right(centre, OCG_GAUGE_CUTOFF, 1 << 30); ++centre; }
+      else { gauge_left(centre, OCG_GAUGE_CUTOFF, 1 << 30); --centre; }
+    }
   }
 
   // ------------------------------------------------------------- step
   // BH_tDMRG::step (src/BH_tDMRG.cpp:111-125) + doStep (:127-230).
-  __device__ void step(double ufrom, double uto, int forward) {
+  // The gate loop is written with one decompose call site and one gauge-move
+  // call site so the (large) decomposition is inlined only twice.
+  __device__ OCG_INLINE void step(double ufrom, double uto, int forward) {
     const int L = P.L, p = P.p;
     const double tau = forward ? P.dt : -P.dt;
     if (tid < p) {
@@ -950,38 +927,29 @@ struct Chain {
       PH[p + tid] = c2(cos(at), sin(at));
     }
     sync();
-    if (L % 2 != 0) site_phase(L, PH);  // lonely U_from on site L
+    if (L % 2 != 0) site_phase(L, PH);  // lonely U_from on site L (:133-136)
     int centre = 1;
     bool movingFromLeft = true;
     for (int g = 0; g < P.ngates; ++g) {
-      int i1 = P.gate_i1[g], i2 = i1 + 1;
+      const int i1 = P.gate_i1[g], i2 = i1 + 1;
       build_theta(i1);
       if (movingFromLeft) apply_gate(i1, forward, 0, (i2 == L && L % 2 == 0) ? 1 : 0);
       else apply_gate(i1, forward, 1, 0);
-      if (g + 1 < P.ngates) {
-        int ni1 = P.gate_i1[g + 1], ni2 = ni1 + 1;
-        if (ni1 >= i2) {
-          decompose(kFromleft, P.cutoff, P.maxm, true, MD + i1 * P.Q1);
-          scatter_two_site(i1);
-          centre = i2;
-          position(centre, ni1);
-        } else {
-          decompose(kFromright, P.cutoff, P.maxm, true, MD + i1 * P.Q1);
-          scatter_two_site(i1);
-          centre = i1;
-          position(centre, ni2);
-        }
-        if (i2 == ni1 || i1 == ni2) movingFromLeft = false;
-      } else {
-        decompose(kFromright, P.cutoff, P.maxm, true, MD + i1 * P.Q1);
-        scatter_two_site(i1);
-        centre = i1;
-        position(centre, 1);
-      }
+      // next gate: right of this one -> Fromleft, centre i2, move to ni1;
+      //            left of it / last -> Fromright, centre i1, move to ni2 / 1
+      const bool more = g + 1 < P.ngates;
+      const int ni1 = more ? P.gate_i1[g + 1] : 0, ni2 = ni1 + 1;
+      const int dir = (more && ni1 >= i2) ? kFromleft : kFromright;
+      decompose(dir, P.cutoff, P.maxm, true, MD + i1 * P.Q1);
+      scatter_two_site(i1);
+      centre = (dir == kFromleft) ? i2 : i1;
+      const int target = !more ? 1 : (dir == kFromleft ? ni1 : ni2);
+      position(centre, target);
+      if (more && (i2 == ni1 || i1 == ni2)) movingFromLeft = false;
     }
-    site_phase(1, PH + p);  // lonely U_to on site 1
+    site_phase(1, PH + p);  // lonely U_to on site 1 (:222-223)
     double n2 = site_norm2(1);
-    if (n2 > 0) site_scale(1, 1.0 / sqrt(n2));
+    if (n2 > 0) site_scale(1, 1.0 / sqrt(n2));  // psi.normalize() (:228)
   }
 
   // ------------------------------------------------------------- overlaps
@@ -992,14 +960,14 @@ struct Chain {
   // (the bond-dimension-2 MPO of propagatorDeriv, src/BH_tDMRG.cpp:10-14).
   // Scratch: G/G2/W/W2 (environments), X (transfer temp), int tables
   // XOFF/YOFF (env offsets), BOFFT (temp offsets), THRO (X block offsets).
-  __device__ double2 overlap(const int* gd, const double2* gx, int with_dH) {
+  __device__ OCG_INLINE zc overlap(const int* gd, const zc* gx, int with_dH) {
     const int p = P.p, Q1 = P.Q1;
-    double2* E0 = G;  double2* E1 = G2;
-    double2* N0 = W;  double2* N1 = W2;
-    int* eo = XOFF;
-    int* no = YOFF;
-    int* to = BOFFT;
-    int* xo = THRO;
+    lzp E0 = G;  lzp E1 = G2;
+    lzp N0 = W;  lzp N1 = W2;
+    LDS int* eo = XOFF;
+    LDS int* no = YOFF;
+    LDS int* to = BOFFT;
+    LDS int* xo = THRO;
     if (tid == 0) {
       eo[0] = 0;
       for (int q = 1; q <= Q1; ++q) eo[q] = 1;  // prefix table: block q=0 is 1x1
@@ -1032,18 +1000,18 @@ struct Chain {
       const int nenv = with_dH ? 2 : 1;
       // T_(q,n) = E_q * Y_(q,n)   for E0 (and E1): rows dX[k-1][q], cols dY[k][q+n]
       for (int ev = 0; ev < nenv; ++ev) {
-        const double2* E = ev == 0 ? E0 : E1;
-        double2* T = X + ev * (P.thcap / 2);
+        lzp E = ev == 0 ? E0 : E1;
+        lzp T = X + ev * (P.thcap / 2);
         for (int q = 0; q < Q1; ++q)
           for (int n = 0; n < p; ++n) {
             int ot = to[q * p + n];
             if (ot < 0) continue;
             int rx = gd[(k - 1) * Q1 + q], ry = d(k - 1, q), cy = d(k, q + n);
-            const double2* Eq = E + eo[q];
-            const double2* Yb = site(k) + bo(k, q, n);
+            lzp Eq = E + eo[q];
+            lzp Yb = site(k) + bo(k, q, n);
             for (int e = tid; e < rx * cy; e += NT) {
               int i = e / cy, j = e - i * cy;
-              double2 acc = c2(0, 0);
+              zc acc = c2(0, 0);
               for (int b = 0; b < ry; ++b) cacc(acc, Eq[i * ry + b], Yb[b * cy + j]);
               T[ot + e] = acc;
             }
@@ -1051,7 +1019,7 @@ struct Chain {
       }
       sync();
       // En_q' = sum_n f(n) X_(q'-n, n)^H T_(q'-n, n)
-      const double2* sx = gx + P.site_base[k];
+      const zc* sx = gx + P.site_base[k];
       const int ne = no[Q1];
       for (int t = tid; t < nenv * ne; t += NT) {
         int ev = t >= ne;
@@ -1060,23 +1028,23 @@ struct Chain {
         int cy = d(k, qq);
         int loc = e - no[qq];
         int a = loc / cy, j = loc - a * cy;
-        double2 acc = c2(0, 0);
+        zc acc = c2(0, 0);
         for (int n = 0; n < p && n <= qq; ++n) {
           int q = qq - n;
           int ot = to[q * p + n];
           if (ot < 0) continue;
           int rx = gd[(k - 1) * Q1 + q], cx = gd[k * Q1 + qq];
-          const double2* Xb = sx + xo[q * p + n];
+          const zc* Xb = sx + xo[q * p + n];
           if (ev == 0) {
-            const double2* Tb = X + ot;
-            double2 s = c2(0, 0);
+            lzp Tb = X + ot;
+            zc s = c2(0, 0);
             for (int i = 0; i < rx; ++i) cjacc(s, Xb[i * cx + a], Tb[i * cy + j]);
             acc = cadd(acc, s);
           } else {
             // E1' = X^H (E1 Y) + f(n) X^H (E0 Y)
-            const double2* T0 = X + ot;
-            const double2* T1 = X + P.thcap / 2 + ot;
-            double2 s0 = c2(0, 0), s1 = c2(0, 0);
+            lzp T0 = X + ot;
+            lzp T1 = X + P.thcap / 2 + ot;
+            zc s0 = c2(0, 0), s1 = c2(0, 0);
             for (int i = 0; i < rx; ++i) {
               cjacc(s1, Xb[i * cx + a], T1[i * cy + j]);
               cjacc(s0, Xb[i * cx + a], T0[i * cy + j]);
@@ -1087,13 +1055,13 @@ struct Chain {
         (ev == 0 ? N0 : N1)[e] = acc;
       }
       sync();
-      double2* t0 = E0; E0 = N0; N0 = t0;
-      double2* t1 = E1; E1 = N1; N1 = t1;
+      lzp t0 = E0; E0 = N0; N0 = t0;
+      lzp t1 = E1; E1 = N1; N1 = t1;
       if (tid == 0)
         for (int q = 0; q <= Q1; ++q) eo[q] = no[q];
       sync();
     }
-    double2 res = c2(0, 0);
+    zc res = c2(0, 0);
     int oq = eo[P.Q];
     if (eo[P.Q1] > oq) res = with_dH ? E1[oq] : E0[oq];
     sync();
@@ -1107,11 +1075,11 @@ struct Chain {
   // right->left with the stepper's Cutoff/Maxm.  In place; the result is
   // right-orthonormal with the (unnormalised) centre at site 1.
   // Carry C_q (new bond k-1 x (s, old bond k-1)) lives in CR at COFF[q].
-  __device__ void apply_dH(bool truncate_sweep = true) {
+  __device__ OCG_INLINE void apply_dH(bool truncate_sweep = true) {
     const int L = P.L, p = P.p, Q1 = P.Q1;
-    int* coff = COFF;   // carry offsets   (Q1+1)
-    int* cdim = CDIM;   // carry rows   = new dims of bond k-1
-    int* cold = COLD;   // carry cols/2 = old dims of bond k-1
+    LDS int* coff = COFF;   // carry offsets   (Q1+1)
+    LDS int* cdim = CDIM;   // carry rows   = new dims of bond k-1
+    LDS int* cold = COLD;   // carry cols/2 = old dims of bond k-1
     if (tid == 0) {
       for (int q = 0; q < Q1; ++q) { cdim[q] = d(0, q); cold[q] = d(0, q); coff[q] = 0; }
       coff[Q1] = 2;
@@ -1155,12 +1123,12 @@ struct Chain {
         int t = last ? 1 : (col >= dc ? 1 : 0);
         int c = last ? col : col - t * dc;
         int dl = cold[ql];                          // old rows of A_k blocks
-        const double2* Ab = site(k) + bo(k, ql, n);  // dl x dc (old layout)
-        const double2* Cq = CR + coff[ql];
+        lzp Ab = site(k) + bo(k, ql, n);  // dl x dc (old layout)
+        lzp Cq = CR + coff[ql];
         int w = 2 * cold[ql];
-        double2 v0 = c2(0, 0), v1 = c2(0, 0);
+        zc v0 = c2(0, 0), v1 = c2(0, 0);
         for (int a = 0; a < dl; ++a) {
-          double2 av = Ab[a * dc + c];
+          zc av = Ab[a * dc + c];
           cacc(v0, Cq[ap * w + a], av);
           cacc(v1, Cq[ap * w + cold[ql] + a], av);
         }

@@ -63,7 +63,7 @@ __device__ inline void flush_stats(const Chain<T>& c, double* stats, double byte
 
 struct Pool {
   int* dims;       // [nslots][nsq]
-  double2* data;   // [nslots][cap]
+  zc* data;   // [nslots][cap]
 };
 
 #define SLOT_D(pool, P, s) ((pool).dims + (size_t)(s) * (P).nsq)
@@ -71,44 +71,42 @@ struct Pool {
 
 // --------------------------------------------------------------------------
 template <int NT>
-__device__ void body_trajectory(char* smem, OcgParams P, const double2* gf, const double2* gb, const int* md,
+__device__ void body_trajectory(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                    Pool pool, int slot_init, int slot_target, int psi_base,
                                                    int xi_base, const double* u, int N, int which, double* stats) {
   Chain<NT> c(P, smem);
   c.load_tables(gf, gb, md);
   int chain = (which == 3) ? blockIdx.x : (which == 1 ? 0 : 1);
+  // chain 0: psi_t forward from psi_init (calcPsi, src/OptimalControl.cpp:375-390)
+  // chain 1: xi_t backward from psi_target (calcXi, :392-407)
+  const int fwd = (chain == 0) ? 1 : 0;
+  const int base = fwd ? psi_base : xi_base;
+  const int src = fwd ? slot_init : slot_target;
   double bytes = 0, flops = 0;
-  if (chain == 0) {
-    c.load(SLOT_D(pool, P, slot_init), SLOT_X(pool, P, slot_init));
-    c.store(SLOT_D(pool, P, psi_base), SLOT_X(pool, P, psi_base));
-    for (int i = 0; i + 1 < N; ++i) {
-      c.step(u[i], u[i + 1], 1);
-      c.store(SLOT_D(pool, P, psi_base + i + 1), SLOT_X(pool, P, psi_base + i + 1));
-      if (threadIdx.x == 0) { double b, f; sweep_model(c, b, f); bytes += b; flops += f; }
-    }
-  } else {
-    c.load(SLOT_D(pool, P, slot_target), SLOT_X(pool, P, slot_target));
-    c.store(SLOT_D(pool, P, xi_base + N - 1), SLOT_X(pool, P, xi_base + N - 1));
-    for (int i = N - 1; i > 0; --i) {
-      c.step(u[i], u[i - 1], 0);
-      c.store(SLOT_D(pool, P, xi_base + i - 1), SLOT_X(pool, P, xi_base + i - 1));
-      if (threadIdx.x == 0) { double b, f; sweep_model(c, b, f); bytes += b; flops += f; }
-    }
+  c.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
+  int t = fwd ? 0 : N - 1;
+  c.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
+  for (int s = 0; s + 1 < N; ++s) {
+    const int tn = fwd ? t + 1 : t - 1;
+    c.step(u[t], u[tn], fwd);
+    c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
+    if (threadIdx.x == 0) { double b, f; sweep_model(c, b, f); bytes += b; flops += f; }
+    t = tn;
   }
   flush_stats(c, stats, bytes, flops, double(N - 1));
 }
 
 // out[i] = <x_i|y_i> or <x_i|dH|y_i>
 template <int NT>
-__device__ void body_overlaps(char* smem, OcgParams P, const double2* gf, const double2* gb, const int* md,
+__device__ void body_overlaps(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                  Pool pool, const int* xs, const int* ys, int npairs, int with_dH,
-                                                 double2* out, double* stats) {
+                                                 zc* out, double* stats) {
   Chain<NT> c(P, smem);
   c.load_tables(gf, gb, md);
   int i = blockIdx.x;
   if (i >= npairs) return;
   c.load(SLOT_D(pool, P, ys[i]), SLOT_X(pool, P, ys[i]));
-  double2 r = c.overlap(SLOT_D(pool, P, xs[i]), SLOT_X(pool, P, xs[i]), with_dH);
+  zc r = c.overlap(SLOT_D(pool, P, xs[i]), SLOT_X(pool, P, xs[i]), with_dH);
   if (threadIdx.x == 0) out[i] = r;
   if (threadIdx.x == 0) {
     double b = 32.0 * mps_nelem(c);
@@ -117,7 +115,7 @@ __device__ void body_overlaps(char* smem, OcgParams P, const double2* gf, const 
 }
 
 template <int NT>
-__device__ void body_apply_dH(char* smem, OcgParams P, const double2* gf, const double2* gb, const int* md,
+__device__ void body_apply_dH(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                  Pool pool, const int* in, const int* outs, int n, double* norms,
                                                  double* stats) {
   Chain<NT> c(P, smem);
@@ -136,45 +134,40 @@ __device__ void body_apply_dH(char* smem, OcgParams P, const double2* gf, const 
   }
 }
 
-// calcHessianRow (src/OptimalControl.cpp:251-279)
+// calcHessianRow (src/OptimalControl.cpp:251-279).  psiH_i =
+// exactApplyMPO(propDeriv, psi_t[i]) and its norm normiH come from a preceding
+// batched body_apply_dH launch (slots psih_base + i, norms[i]).
 template <int NT>
-__device__ void body_hessian_rows(char* smem, OcgParams P, const double2* gf, const double2* gb,
-                                                     const int* md, Pool pool, int psi_base, int xih_base,
-                                                     const int* rows, int nrows, const double* u, int N,
-                                                     const double2* divT, double2 F, double* H, double* stats) {
+__device__ void body_hessian_rows(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md, Pool pool,
+                                  int psih_base, int xih_base, const int* rows, int nrows, const double* norms,
+                                  const double* u, int N, const zc* divT, zc F, double* H, double* stats) {
   Chain<NT> c(P, smem);
   c.load_tables(gf, gb, md);
   int r = blockIdx.x;
   if (r >= nrows) return;
   const int i = rows[r];
   const double dt2 = P.dt * P.dt;
-  c.load(SLOT_D(pool, P, psi_base + i), SLOT_X(pool, P, psi_base + i));
-  c.apply_dH();  // psiH = exactApplyMPO(propDeriv, psi_t[i], args)
-  const double normiH = sqrt(c.site_norm2(1));
+  const double normiH = norms[i];
+  c.load(SLOT_D(pool, P, psih_base + i), SLOT_X(pool, P, psih_base + i));
   double bytes = 0, flops = 0;
-  {
-    double2 ov = c.overlap(SLOT_D(pool, P, xih_base + i), SLOT_X(pool, P, xih_base + i), 0);
+  // j = i: diagonal entry (:259-264); j > i: step psiH once, then overlap (:266-278)
+  for (int j = i; j + 1 < N; ++j) {
+    if (j > i) c.step(u[j - 1], u[j], 1);
+    zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
     if (threadIdx.x == 0) {
-      double2 dv = divT[i];
-      double v1 = F.x * ov.x - F.y * ov.y;          // Re(F <xiH_i|psiH>)
-      double v2 = -(dv.x * dv.x + dv.y * dv.y);     // -|divT_i|^2
-      H[(size_t)i * N + i] = dt2 * (v1 + v2);
-    }
-  }
-  for (int j = i + 1; j + 1 < N; ++j) {
-    c.step(u[j - 1], u[j], 1);
-    double2 ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
-    if (threadIdx.x == 0) {
-      double2 di = divT[i], dj = divT[j];
-      double v1 = (F.x * ov.x - F.y * ov.y) * normiH;   // Re(F <xiH_j|psiH> n_i)
-      double v2 = -(di.x * dj.x + di.y * dj.y);          // -Re(divT_i conj(divT_j))
+      zc di = divT[i], dj = divT[j];
+      double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? normiH : 1.0);  // Re(F <xiH_j|psiH> n_i)
+      double v2 = -(di.x * dj.x + di.y * dj.y);                        // -Re(divT_i conj(divT_j))
       double res = dt2 * (v1 + v2);
       H[(size_t)i * N + j] = res;
-      H[(size_t)j * N + i] = res;
-      double b, f;
-      sweep_model(c, b, f);
-      bytes += b + 32.0 * mps_nelem(c);
-      flops += f;
+      if (j > i) H[(size_t)j * N + i] = res;
+      if (j > i) {
+        double b, f;
+        sweep_model(c, b, f);
+        bytes += b;
+        flops += f;
+      }
+      bytes += 32.0 * mps_nelem(c);
     }
   }
   flush_stats(c, stats, bytes, flops, double(N - 2 - i > 0 ? N - 2 - i : 0));
@@ -182,7 +175,7 @@ __device__ void body_hessian_rows(char* smem, OcgParams P, const double2* gf, co
 
 // nsteps steps per state; u holds nsteps+1 controls per state (u_stride apart)
 template <int NT>
-__device__ void body_steps(char* smem, OcgParams P, const double2* gf, const double2* gb, const int* md,
+__device__ void body_steps(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
                                               Pool pool, const int* slots, int n, const double* u, int u_stride,
                                               int nsteps, int forward, double* stats) {
   Chain<NT> c(P, smem);

@@ -22,6 +22,8 @@
 #include "params.hpp"
 
 using ocg::Chain;
+using ocg::zc;
+static inline zc mkz(double x, double y) { zc r; r.x = x; r.y = y; return r; }
 
 #ifndef OCG_NT
 #define OCG_NT 64
@@ -33,36 +35,37 @@ using ocg::Pool;
 
 // --------------------------------------------------------------------------
 // __global__ entry points
-__global__ __launch_bounds__(NT) void k_trajectory(OcgParams P, const double2* gf, const double2* gb, const int* md,
+__global__ __launch_bounds__(NT) void k_trajectory(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                    Pool pool, int slot_init, int slot_target, int psi_base,
                                                    int xi_base, const double* u, int N, int which, double* stats) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_trajectory<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, u, N, which, stats);
 }
 
-__global__ __launch_bounds__(NT) void k_overlaps(OcgParams P, const double2* gf, const double2* gb, const int* md,
+__global__ __launch_bounds__(NT) void k_overlaps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                  Pool pool, const int* xs, const int* ys, int npairs, int with_dH,
-                                                 double2* out, double* stats) {
+                                                 zc* out, double* stats) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_overlaps<NT>(smem, P, gf, gb, md, pool, xs, ys, npairs, with_dH, out, stats);
 }
 
-__global__ __launch_bounds__(NT) void k_apply_dH(OcgParams P, const double2* gf, const double2* gb, const int* md,
+__global__ __launch_bounds__(NT) void k_apply_dH(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                  Pool pool, const int* in, const int* outs, int n, double* norms,
                                                  double* stats) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_apply_dH<NT>(smem, P, gf, gb, md, pool, in, outs, n, norms, stats);
 }
 
-__global__ __launch_bounds__(NT) void k_hessian_rows(OcgParams P, const double2* gf, const double2* gb,
-                                                     const int* md, Pool pool, int psi_base, int xih_base,
-                                                     const int* rows, int nrows, const double* u, int N,
-                                                     const double2* divT, double2 F, double* H, double* stats) {
+__global__ __launch_bounds__(NT) void k_hessian_rows(OcgParams P, const zc* gf, const zc* gb, const int* md,
+                                                     Pool pool, int psih_base, int xih_base, const int* rows,
+                                                     int nrows, const double* norms, const double* u, int N,
+                                                     const zc* divT, zc F, double* H, double* stats) {
   extern __shared__ __align__(16) char smem[];
-  ocg::body_hessian_rows<NT>(smem, P, gf, gb, md, pool, psi_base, xih_base, rows, nrows, u, N, divT, F, H, stats);
+  ocg::body_hessian_rows<NT>(smem, P, gf, gb, md, pool, psih_base, xih_base, rows, nrows, norms, u, N, divT, F, H,
+                             stats);
 }
 
-__global__ __launch_bounds__(NT) void k_steps(OcgParams P, const double2* gf, const double2* gb, const int* md,
+__global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                               Pool pool, const int* slots, int n, const double* u, int u_stride,
                                               int nsteps, int forward, double* stats) {
   extern __shared__ __align__(16) char smem[];
@@ -92,7 +95,7 @@ struct ocg_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // device buffers
-  double2 *d_gf = nullptr, *d_gb = nullptr;
+  zc *d_gf = nullptr, *d_gb = nullptr;
   int* d_md = nullptr;
   Pool pool{nullptr, nullptr};
   int nslots = 0;
@@ -101,11 +104,15 @@ struct ocg_ctx {
   int idx_cap = 0;
   double* d_u = nullptr;
   int u_cap = 0;
-  double2* d_c = nullptr;     // complex scratch (overlaps / divT)
+  zc* d_c = nullptr;     // complex scratch (overlaps / divT)
   int c_cap = 0;
   double* d_H = nullptr;
   size_t H_cap = 0;
   double* d_norms = nullptr;
+  double* d_rnorm = nullptr;  // psiH norms (by row index)
+  int rnorm_cap = 0;
+  int* d_idx2 = nullptr;      // index scratch of the psiH launch
+  int idx2_cap = 0;
   // trajectory state
   int N = 0;
   bool have_states = false, have_psi = false, have_xi = false, have_xih = false;
@@ -117,6 +124,7 @@ struct ocg_ctx {
   int psi_base() const { return 6; }
   int xi_base() const { return 6 + N; }
   int xih_base() const { return 6 + 2 * N; }
+  int psih_base() const { return 6 + 3 * N; }
 };
 
 #define HIPCHK(ctx, expr)                                                               \
@@ -138,11 +146,11 @@ static int upload_gates(ocg_ctx* c) {
   ocg_host::gate_tables(c->P, c->J, gf, gb);
   const int off = c->P.gtotal;
   if (!c->d_gf) {
-    HIPCHK(c, hipMalloc(&c->d_gf, sizeof(double2) * off));
-    HIPCHK(c, hipMalloc(&c->d_gb, sizeof(double2) * off));
+    HIPCHK(c, hipMalloc(&c->d_gf, sizeof(zc) * off));
+    HIPCHK(c, hipMalloc(&c->d_gb, sizeof(zc) * off));
   }
-  HIPCHK(c, hipMemcpy(c->d_gf, gf.data(), sizeof(double2) * off, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_gb, gb.data(), sizeof(double2) * off, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_gf, gf.data(), sizeof(zc) * off, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_gb, gb.data(), sizeof(zc) * off, hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -156,13 +164,13 @@ static int ensure_slots(ocg_ctx* c, int nslots) {
   if (nslots <= c->nslots) return 0;
   int n = std::max(nslots, 2 * c->nslots);
   int* nd = nullptr;
-  double2* nx = nullptr;
+  zc* nx = nullptr;
   HIPCHK(c, hipMalloc(&nd, sizeof(int) * size_t(n) * c->P.nsq));
-  HIPCHK(c, hipMalloc(&nx, sizeof(double2) * size_t(n) * c->P.cap));
+  HIPCHK(c, hipMalloc(&nx, sizeof(zc) * size_t(n) * c->P.cap));
   HIPCHK(c, hipMemset(nd, 0, sizeof(int) * size_t(n) * c->P.nsq));
   if (c->nslots) {
     HIPCHK(c, hipMemcpy(nd, c->pool.dims, sizeof(int) * size_t(c->nslots) * c->P.nsq, hipMemcpyDeviceToDevice));
-    HIPCHK(c, hipMemcpy(nx, c->pool.data, sizeof(double2) * size_t(c->nslots) * c->P.cap,
+    HIPCHK(c, hipMemcpy(nx, c->pool.data, sizeof(zc) * size_t(c->nslots) * c->P.cap,
                         hipMemcpyDeviceToDevice));
     (void)hipFree(c->pool.dims);
     (void)hipFree(c->pool.data);
@@ -214,16 +222,16 @@ static int validate_dims(ocg_ctx* c, const int* dims) {
 static int upload_mps(ocg_ctx* c, int slot, const int* dims, const double* data) {
   const OcgParams& P = c->P;
   if (int rc = validate_dims(c, dims)) return rc;
-  std::vector<double2> buf(P.cap, make_double2(0, 0));
+  std::vector<zc> buf(P.cap, mkz(0, 0));
   size_t off = 0;
   for (int k = 1; k <= P.L; ++k) {
     size_t n = nelem_of(P, dims, k);
     if (n > size_t(P.site_cap[k])) return fail(c, OCG_ECAP, "site tensor exceeds capacity");
-    for (size_t i = 0; i < n; ++i) buf[P.site_base[k] + i] = make_double2(data[2 * (off + i)], data[2 * (off + i) + 1]);
+    for (size_t i = 0; i < n; ++i) buf[P.site_base[k] + i] = mkz(data[2 * (off + i)], data[2 * (off + i) + 1]);
     off += n;
   }
   HIPCHK(c, hipMemcpyAsync(SLOT_D(c->pool, P, slot), dims, sizeof(int) * P.nsq, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(SLOT_X(c->pool, P, slot), buf.data(), sizeof(double2) * P.cap, hipMemcpyHostToDevice,
+  HIPCHK(c, hipMemcpyAsync(SLOT_X(c->pool, P, slot), buf.data(), sizeof(zc) * P.cap, hipMemcpyHostToDevice,
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
@@ -232,9 +240,9 @@ static int upload_mps(ocg_ctx* c, int slot, const int* dims, const double* data)
 static int download_mps(ocg_ctx* c, int slot, int* dims, double* data, size_t cap, size_t* nelem) {
   const OcgParams& P = c->P;
   std::vector<int> d(P.nsq);
-  std::vector<double2> buf(P.cap);
+  std::vector<zc> buf(P.cap);
   HIPCHK(c, hipMemcpyAsync(d.data(), SLOT_D(c->pool, P, slot), sizeof(int) * P.nsq, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(buf.data(), SLOT_X(c->pool, P, slot), sizeof(double2) * P.cap, hipMemcpyDeviceToHost,
+  HIPCHK(c, hipMemcpyAsync(buf.data(), SLOT_X(c->pool, P, slot), sizeof(zc) * P.cap, hipMemcpyDeviceToHost,
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   size_t tot = 0;
@@ -280,6 +288,7 @@ static int set_lds(ocg_ctx* c) {
 }
 
 static int finish_params(ocg_ctx* c) {
+  if (c->P.gtotal <= 0) return fail(c, OCG_ESTATE, "internal: gate tables must be built before the LDS layout");
   ocg::LdsLayout l = ocg::lds_layout(c->P, NT);
   c->P.lds_bytes = l.bytes;
   hipDeviceProp_t prop;
@@ -327,13 +336,14 @@ int ocg_create(int device, int L, int p, int npart, double J, double tstep, doub
   }
   if (device < 0 || device >= ndev) { c->err = "device index out of range"; return bail(OCG_EINVAL); }
   if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(OCG_EHIP); }
+  // gate tables first: their size (gtotal) is part of the LDS layout
+  if ((rc = upload_gates(c))) return bail(rc);
   if ((rc = finish_params(c))) return bail(rc);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     c->err = "stream/event creation failed";
     return bail(OCG_EHIP);
   }
-  if ((rc = upload_gates(c))) return bail(rc);
   if (hipMalloc(&c->d_md, sizeof(int) * c->md.size()) != hipSuccess ||
       hipMemcpy(c->d_md, c->md.data(), sizeof(int) * c->md.size(), hipMemcpyHostToDevice) != hipSuccess ||
       hipMalloc(&c->d_stats, sizeof(double) * 15) != hipSuccess ||
@@ -361,6 +371,8 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->d_c) (void)hipFree(c->d_c);
   if (c->d_H) (void)hipFree(c->d_H);
   if (c->d_norms) (void)hipFree(c->d_norms);
+  if (c->d_rnorm) (void)hipFree(c->d_rnorm);
+  if (c->d_idx2) (void)hipFree(c->d_idx2);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -416,7 +428,7 @@ int ocg_step(ocg_ctx* c, const int* dims, const double* data, double from, doubl
 }
 
 static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::vector<int>& ys, int with_dH,
-                           std::vector<double2>& out) {
+                           std::vector<zc>& out) {
   const OcgParams& P = c->P;
   int n = int(xs.size());
   if (n == 0) return 0;
@@ -430,7 +442,7 @@ static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::ve
                      c->d_idx, c->d_idx + n, n, with_dH, c->d_c, c->d_stats + 1 * 3);
   if (int rc = end_kernel(c, 1)) return rc;
   out.resize(n);
-  HIPCHK(c, hipMemcpy(out.data(), c->d_c, sizeof(double2) * n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(out.data(), c->d_c, sizeof(zc) * n, hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -440,7 +452,7 @@ int ocg_overlap(ocg_ctx* c, const int* dims_x, const double* x, const int* dims_
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = upload_mps(c, c->slot_tmp(0), dims_x, x)) return rc;
   if (int rc = upload_mps(c, c->slot_tmp(1), dims_y, y)) return rc;
-  std::vector<double2> r;
+  std::vector<zc> r;
   if (int rc = launch_overlaps(c, {c->slot_tmp(0)}, {c->slot_tmp(1)}, with_dH, r)) return rc;
   out[0] = r[0].x;
   out[1] = r[0].y;
@@ -454,6 +466,8 @@ static int launch_apply_dH(ocg_ctx* c, const std::vector<int>& in, const std::ve
   int ncap = 0;
   if (norms) {
     if (c->d_norms) (void)hipFree(c->d_norms);
+  if (c->d_rnorm) (void)hipFree(c->d_rnorm);
+  if (c->d_idx2) (void)hipFree(c->d_idx2);
     c->d_norms = nullptr;
     if (int rc = ensure_buf(c, c->d_norms, ncap, n)) return rc;
   }
@@ -499,7 +513,7 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
     c->N = N;
     c->have_psi = c->have_xi = c->have_xih = false;
   }
-  if (int rc = ensure_slots(c, 6 + 3 * N)) return rc;
+  if (int rc = ensure_slots(c, 6 + 4 * N)) return rc;
   if (int rc = ensure_buf(c, c->d_u, c->u_cap, N)) return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
   int grid = (which == 3) ? 2 : 1;
@@ -517,7 +531,7 @@ int ocg_overlap_factor(ocg_ctx* c, double* F) {
   if (!c || !F) return OCG_EINVAL;
   if (!c->have_psi) return fail(c, OCG_ESTATE, "psi_t not propagated");
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<double2> r;
+  std::vector<zc> r;
   // overlapC(psi_t.back(), psi_target) = <psi_T|target>
   if (int rc = launch_overlaps(c, {c->psi_base() + c->N - 1}, {c->slot_target()}, 0, r)) return rc;
   F[0] = r[0].x;
@@ -531,7 +545,7 @@ int ocg_fidelities(ocg_ctx* c, double* fid) {
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<int> xs(c->N, c->slot_target()), ys(c->N);
   for (int i = 0; i < c->N; ++i) ys[i] = c->psi_base() + i;
-  std::vector<double2> r;
+  std::vector<zc> r;
   if (int rc = launch_overlaps(c, xs, ys, 0, r)) return rc;
   for (int i = 0; i < c->N; ++i) fid[i] = r[i].x * r[i].x + r[i].y * r[i].y;
   return 0;
@@ -543,7 +557,7 @@ int ocg_div_t(ocg_ctx* c, double* divT) {
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<int> xs(c->N), ys(c->N);
   for (int i = 0; i < c->N; ++i) { xs[i] = c->xi_base() + i; ys[i] = c->psi_base() + i; }
-  std::vector<double2> r;
+  std::vector<zc> r;
   if (int rc = launch_overlaps(c, xs, ys, 1, r)) return rc;
   for (int i = 0; i < c->N; ++i) { divT[2 * i] = r[i].x; divT[2 * i + 1] = r[i].y; }
   return 0;
@@ -580,13 +594,31 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
   }
   HIPCHK(c, hipMemcpyAsync(c->d_idx, rows, sizeof(int) * nrows, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_c, divT, sizeof(double2) * N, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_c, divT, sizeof(zc) * N, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
-  double2 f2 = make_double2(F[0], F[1]);
+  // psiH_i = exactApplyMPO(propDeriv, psi_t[i]) and normiH for the requested rows
+  {
+    std::vector<int> in(nrows), outs(nrows);
+    for (int r = 0; r < nrows; ++r) { in[r] = c->psi_base() + rows[r]; outs[r] = c->psih_base() + rows[r]; }
+    if (int rc = ensure_buf(c, c->d_rnorm, c->rnorm_cap, N)) return rc;
+    if (int rc = ensure_buf(c, c->d_idx2, c->idx2_cap, 2 * nrows)) return rc;
+    in.insert(in.end(), outs.begin(), outs.end());
+    HIPCHK(c, hipMemcpyAsync(c->d_idx2, in.data(), sizeof(int) * 2 * nrows, hipMemcpyHostToDevice, c->stream));
+    if (int rc = begin_kernel(c)) return rc;
+    hipLaunchKernelGGL(k_apply_dH, dim3(nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+                       c->pool, c->d_idx2, c->d_idx2 + nrows, nrows, c->d_rnorm, c->d_stats + 2 * 3);
+    if (int rc = end_kernel(c, 2)) return rc;
+    // k_apply_dH writes norms[r] (row order); scatter to index i on the host side of the rows kernel
+    std::vector<double> nr(nrows), ni(N, 0.0);
+    HIPCHK(c, hipMemcpy(nr.data(), c->d_rnorm, sizeof(double) * nrows, hipMemcpyDeviceToHost));
+    for (int r = 0; r < nrows; ++r) ni[rows[r]] = nr[r];
+    HIPCHK(c, hipMemcpy(c->d_rnorm, ni.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+  }
+  zc f2 = mkz(F[0], F[1]);
   if (int rc = begin_kernel(c)) return rc;
   hipLaunchKernelGGL(k_hessian_rows, dim3(nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
-                     c->pool, c->psi_base(), c->xih_base(), c->d_idx, nrows, c->d_u, N, c->d_c, f2, c->d_H,
-                     c->d_stats + 3 * 3);
+                     c->pool, c->psih_base(), c->xih_base(), c->d_idx, nrows, c->d_rnorm, c->d_u, N, c->d_c, f2,
+                     c->d_H, c->d_stats + 3 * 3);
   if (int rc = end_kernel(c, 3)) return rc;
   std::vector<double> h(hn);
   HIPCHK(c, hipMemcpy(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost));

@@ -1,0 +1,263 @@
+"""ctypes binding of liboptimalcontrolmps_amd.so (include/ocmps.h).
+
+The shared library is built in-tree (``build_native()``, also run by
+``__graft_entry__.build()``) with hipcc for gfx950 and lives next to this
+file.  There is no fallback: if the library is missing or the HIP runtime has
+no GPU, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+LIB_NAME = "liboptimalcontrolmps_amd.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+CSRC = os.path.join(PKG_DIR, "csrc")
+HEADER = os.path.join(ROOT, "include", "ocmps.h")
+
+OCG_ERRORS = {1: "EINVAL", 2: "ECAP", 3: "EHIP", 4: "ESTATE", 5: "ENUM"}
+
+
+class OcgError(RuntimeError):
+    pass
+
+
+def sources():
+    return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))
+            if f.endswith((".hip", ".hpp", ".cpp", ".h"))] + [HEADER]
+
+
+def build_native(force: bool = False, nt: int | None = None, verbose: bool = False) -> str:
+    """Compile csrc/ocmps.hip into the in-tree shared library (gfx950)."""
+    if not force and os.path.exists(LIB_PATH):
+        newest = max(os.path.getmtime(s) for s in sources())
+        if os.path.getmtime(LIB_PATH) >= newest:
+            return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-o", LIB_PATH + ".tmp", os.path.join(CSRC, "ocmps.hip")]
+    if nt:
+        cmd.insert(1, f"-DOCG_NT={int(nt)}")
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+dp = C.POINTER(C.c_double)
+ip = C.POINTER(C.c_int)
+szp = C.POINTER(C.c_size_t)
+
+
+class OcgInfo(C.Structure):
+    _fields_ = [("L", C.c_int), ("p", C.c_int), ("Q", C.c_int), ("mps_max_nelem", C.c_size_t),
+                ("lds_bytes", C.c_int), ("block_threads", C.c_int), ("device", C.c_int)]
+
+
+# (name, restype, argtypes) for every entry point of include/ocmps.h
+SIGNATURES = [
+    ("ocg_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
+                             C.POINTER(C.c_void_p)]),
+    ("ocg_destroy", C.c_int, [C.c_void_p]),
+    ("ocg_last_error", C.c_char_p, [C.c_void_p]),
+    ("ocg_get_info", C.c_int, [C.c_void_p, C.POINTER(OcgInfo)]),
+    ("ocg_set_tstep", C.c_int, [C.c_void_p, C.c_double]),
+    ("ocg_mps_nelem", C.c_size_t, [C.c_int, C.c_int, C.c_int, ip]),
+    ("ocg_step", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_steps", C.c_int, [C.c_void_p, ip, dp, dp, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_overlap", C.c_int, [C.c_void_p, ip, dp, ip, dp, C.c_int, dp]),
+    ("ocg_apply_dH", C.c_int, [C.c_void_p, ip, dp, ip, dp, C.c_size_t, szp, dp]),
+    ("ocg_set_states", C.c_int, [C.c_void_p, ip, dp, ip, dp]),
+    ("ocg_propagate", C.c_int, [C.c_void_p, dp, C.c_int, C.c_int]),
+    ("ocg_overlap_factor", C.c_int, [C.c_void_p, dp]),
+    ("ocg_fidelities", C.c_int, [C.c_void_p, dp]),
+    ("ocg_div_t", C.c_int, [C.c_void_p, dp]),
+    ("ocg_xi_dH", C.c_int, [C.c_void_p]),
+    ("ocg_hessian_rows", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
+    ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_kernel_stats", C.c_int, [C.c_void_p, C.c_int, dp, C.POINTER(C.c_long), dp, dp, C.POINTER(C.c_long)]),
+    ("ocg_reset_stats", C.c_int, [C.c_void_p]),
+]
+
+
+def lib():
+    """Load the native library (raises OcgError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OcgError(f"{LIB_NAME} not built: run optimalcontrolmps_amd.native.build_native() "
+                           "or __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(dp)
+
+
+def _i(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return a, a.ctypes.data_as(ip)
+
+
+class MPS:
+    """Host MPS in the compact U(1)-block interchange format of include/ocmps.h
+    (the IQMPS replacement): dims int32[(L+1)*(Q+1)], data complex128."""
+
+    def __init__(self, L, p, Q, dims, data):
+        self.L, self.p, self.Q = int(L), int(p), int(Q)
+        self.dims = np.ascontiguousarray(np.asarray(dims, dtype=np.int32).reshape(-1))
+        self.data = np.ascontiguousarray(np.asarray(data, dtype=np.complex128).reshape(-1))
+
+    def bond_dims(self):
+        return self.dims.reshape(self.L + 1, self.Q + 1).sum(axis=1)
+
+    def raw(self):
+        return self.data.view(np.float64)
+
+    def copy(self):
+        return MPS(self.L, self.p, self.Q, self.dims.copy(), self.data.copy())
+
+
+class Engine:
+    """One device context (ocg_ctx): the BH_tDMRG stepper + device-resident
+    trajectories of the OptimalControl hot path."""
+
+    def __init__(self, L, p, npart, J, tstep, cutoff, maxm=0, device=0):
+        self.L, self.p, self.Q = L, p, npart
+        self.J, self.tstep, self.cutoff, self.maxm = J, tstep, cutoff, maxm
+        h = C.c_void_p()
+        rc = lib().ocg_create(device, L, p, npart, J, tstep, cutoff, maxm, C.byref(h))
+        if rc != 0:
+            raise OcgError(f"ocg_create failed ({OCG_ERRORS.get(rc, rc)}): "
+                           f"{lib().ocg_last_error(None).decode()}")
+        self.h = h
+        info = OcgInfo()
+        lib().ocg_get_info(self.h, C.byref(info))
+        self.info = info
+        self.cap = int(info.mps_max_nelem)
+        self.N = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ocg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise OcgError(f"{what} failed ({OCG_ERRORS.get(rc, rc)}): {lib().ocg_last_error(self.h).decode()}")
+
+    def _out(self):
+        return (np.zeros((self.L + 1) * (self.Q + 1), np.int32), np.zeros(2 * self.cap), C.c_size_t(0))
+
+    def _wrap(self, fd, d, n):
+        return MPS(self.L, self.p, self.Q, fd.copy(), d[:2 * n.value].view(np.complex128).copy())
+
+    # ------------------------------------------------ TimeStepper-level
+    def step(self, m: MPS, u_from, u_to, forward=True) -> MPS:
+        fd, d, n = self._out()
+        _, pd = _i(m.dims)
+        raw, pr = _d(m.raw())
+        self._chk(lib().ocg_step(self.h, pd, pr, u_from, u_to, int(forward), fd.ctypes.data_as(ip),
+                                 d.ctypes.data_as(dp), self.cap, C.byref(n)), "ocg_step")
+        return self._wrap(fd, d, n)
+
+    def steps(self, m: MPS, u, forward=True) -> MPS:
+        fd, d, n = self._out()
+        _, pd = _i(m.dims)
+        raw, pr = _d(m.raw())
+        uu, pu = _d(u)
+        self._chk(lib().ocg_steps(self.h, pd, pr, pu, len(uu) - 1, int(forward), fd.ctypes.data_as(ip),
+                                  d.ctypes.data_as(dp), self.cap, C.byref(n)), "ocg_steps")
+        return self._wrap(fd, d, n)
+
+    def overlap(self, x: MPS, y: MPS, with_dH=False) -> complex:
+        out = np.zeros(2)
+        _, a = _i(x.dims); rx, b = _d(x.raw()); _, c = _i(y.dims); ry, d = _d(y.raw())
+        self._chk(lib().ocg_overlap(self.h, a, b, c, d, int(with_dH), out.ctypes.data_as(dp)), "ocg_overlap")
+        return complex(out[0], out[1])
+
+    def apply_dH(self, m: MPS):
+        fd, d, n = self._out()
+        nrm = C.c_double(0)
+        _, pd = _i(m.dims)
+        raw, pr = _d(m.raw())
+        self._chk(lib().ocg_apply_dH(self.h, pd, pr, fd.ctypes.data_as(ip), d.ctypes.data_as(dp), self.cap,
+                                     C.byref(n), C.byref(nrm)), "ocg_apply_dH")
+        return self._wrap(fd, d, n), nrm.value
+
+    # ------------------------------------------------ OptimalControl hot path
+    def set_states(self, target: MPS, init: MPS):
+        _, a = _i(target.dims); rt, b = _d(target.raw()); _, c = _i(init.dims); ri, d = _d(init.raw())
+        self._chk(lib().ocg_set_states(self.h, a, b, c, d), "ocg_set_states")
+
+    def propagate(self, u, which=3):
+        uu, pu = _d(u)
+        self.N = len(uu)
+        self._chk(lib().ocg_propagate(self.h, pu, len(uu), which), "ocg_propagate")
+
+    def overlap_factor(self) -> complex:
+        out = np.zeros(2)
+        self._chk(lib().ocg_overlap_factor(self.h, out.ctypes.data_as(dp)), "ocg_overlap_factor")
+        return complex(out[0], out[1])
+
+    def fidelities(self):
+        out = np.zeros(self.N)
+        self._chk(lib().ocg_fidelities(self.h, out.ctypes.data_as(dp)), "ocg_fidelities")
+        return out
+
+    def div_t(self):
+        out = np.zeros(2 * self.N)
+        self._chk(lib().ocg_div_t(self.h, out.ctypes.data_as(dp)), "ocg_div_t")
+        return out.view(np.complex128).copy()
+
+    def xi_dH(self):
+        self._chk(lib().ocg_xi_dH(self.h), "ocg_xi_dH")
+
+    def hessian_rows(self, u, rows, F: complex, divT, H=None):
+        uu, pu = _d(u)
+        N = len(uu)
+        r, pr = _i(rows)
+        Fa = np.array([F.real, F.imag])
+        dv = np.ascontiguousarray(np.asarray(divT, np.complex128)).view(np.float64)
+        if H is None:
+            H = np.zeros((N, N))
+        H = np.ascontiguousarray(H, dtype=np.float64)
+        self._chk(lib().ocg_hessian_rows(self.h, pu, N, pr, len(r), Fa.ctypes.data_as(dp), dv.ctypes.data_as(dp),
+                                         H.ctypes.data_as(dp)), "ocg_hessian_rows")
+        return H
+
+    def state(self, which, t) -> MPS:
+        fd, d, n = self._out()
+        self._chk(lib().ocg_get_state(self.h, which, t, fd.ctypes.data_as(ip), d.ctypes.data_as(dp), self.cap,
+                                      C.byref(n)), "ocg_get_state")
+        return self._wrap(fd, d, n)
+
+    def stats(self, kind):
+        ms = C.c_double(); n = C.c_long(); b = C.c_double(); f = C.c_double(); s = C.c_long()
+        self._chk(lib().ocg_kernel_stats(self.h, kind, C.byref(ms), C.byref(n), C.byref(b), C.byref(f),
+                                         C.byref(s)), "ocg_kernel_stats")
+        return {"ms": ms.value, "launches": n.value, "alg_bytes": b.value, "alg_flops": f.value,
+                "sweep_steps": s.value}
+
+    def reset_stats(self):
+        self._chk(lib().ocg_reset_stats(self.h), "ocg_reset_stats")

@@ -24,23 +24,23 @@ struct Emu {
   std::vector<double> gf, gb;
   int lds = 0;
   std::vector<int> dims;       // pool
-  std::vector<double2> data;
+  std::vector<ocg::zc> data;
   int nslots = 0;
   double stats[15] = {0};
   void slots(int n) {
     if (n <= nslots) return;
     dims.resize(size_t(n) * P.nsq, 0);
-    data.resize(size_t(n) * P.cap, double2{0, 0});
+    data.resize(size_t(n) * P.cap, ocg::c2(0, 0));
     nslots = n;
   }
   ocg::Pool pool() { return ocg::Pool{dims.data(), data.data()}; }
-  const double2* GF() { return reinterpret_cast<const double2*>(gf.data()); }
-  const double2* GB() { return reinterpret_cast<const double2*>(gb.data()); }
+  const ocg::zc* GF() { return reinterpret_cast<const ocg::zc*>(gf.data()); }
+  const ocg::zc* GB() { return reinterpret_cast<const ocg::zc*>(gb.data()); }
 };
 
 static void launch(Emu& e, int grid, const std::function<void(char*)>& body) {
   for (int b = 0; b < grid; ++b) {
-    std::vector<double2> smem((e.lds + 15) / 16 + 1);
+    std::vector<ocg::zc> smem((e.lds + 15) / 16 + 1);
     std::barrier<> bar(NT);
     std::vector<std::thread> th;
     for (int t = 0; t < NT; ++t)
@@ -67,7 +67,7 @@ static void put(Emu& e, int slot, const int* dims, const double* x) {
   for (int k = 1; k <= P.L; ++k) {
     size_t n = nelem_site(P, dims, k);
     for (size_t i = 0; i < n; ++i)
-      e.data[size_t(slot) * P.cap + P.site_base[k] + i] = double2{x[2 * (off + i)], x[2 * (off + i) + 1]};
+      e.data[size_t(slot) * P.cap + P.site_base[k] + i] = ocg::c2(x[2 * (off + i)], x[2 * (off + i) + 1]);
     off += n;
   }
 }
@@ -79,7 +79,7 @@ static size_t get(Emu& e, int slot, int* dims, double* x) {
   for (int k = 1; k <= P.L; ++k) {
     size_t n = nelem_site(P, d, k);
     for (size_t i = 0; i < n; ++i) {
-      double2 z = e.data[size_t(slot) * P.cap + P.site_base[k] + i];
+      ocg::zc z = e.data[size_t(slot) * P.cap + P.site_base[k] + i];
       x[2 * (off + i)] = z.x;
       x[2 * (off + i) + 1] = z.y;
     }
@@ -133,7 +133,7 @@ void emu_overlap(void* h, const int* dx, const double* x, const int* dy, const d
   put(e, 2, dx, x);
   put(e, 3, dy, y);
   int xs = 2, ys = 3;
-  double2 r{0, 0};
+  ocg::zc r = ocg::c2(0, 0);
   OcgParams P = e.P;
   launch(e, 1, [&](char* smem) {
     ocg::body_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), &xs, &ys, 1, with_dH, &r, e.stats + 3);
@@ -155,7 +155,7 @@ void emu_hessian(void* h, const int* dt_, const double* tgt, const int* di, cons
     ocg::body_trajectory<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, u, N, 3, e.stats);
   });
   std::vector<int> xs(N), ys(N);
-  std::vector<double2> r(N);
+  std::vector<ocg::zc> r(N);
   for (int i = 0; i < N; ++i) { xs[i] = xi + i; ys[i] = psi + i; }
   launch(e, N, [&](char* smem) {
     ocg::body_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), xs.data(), ys.data(), N, 1, r.data(),
@@ -169,7 +169,7 @@ void emu_hessian(void* h, const int* dt_, const double* tgt, const int* di, cons
   });
   for (int i = 0; i < N; ++i) fid[i] = r[i].x * r[i].x + r[i].y * r[i].y;
   int a = psi + N - 1, b = 1;
-  double2 f{0, 0};
+  ocg::zc f = ocg::c2(0, 0);
   launch(e, 1, [&](char* smem) {
     ocg::body_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), &a, &b, 1, 0, &f, e.stats + 3);
   });
@@ -183,12 +183,22 @@ void emu_hessian(void* h, const int* dt_, const double* tgt, const int* di, cons
   });
   std::vector<int> rows;
   for (int i = 1; i + 1 < N && int(rows.size()) < nrows_max; ++i) rows.push_back(i);
-  std::vector<double2> dv(N);
-  for (int i = 0; i < N; ++i) dv[i] = double2{divT[2 * i], divT[2 * i + 1]};
+  std::vector<ocg::zc> dv(N);
+  for (int i = 0; i < N; ++i) dv[i] = ocg::c2(divT[2 * i], divT[2 * i + 1]);
   std::memset(H, 0, sizeof(double) * N * N);
+  e.slots(6 + 4 * N);
+  const int psih = 6 + 3 * N;
+  std::vector<int> pin(rows.size()), pout(rows.size());
+  std::vector<double> nr(rows.size()), ni(N, 0.0);
+  for (size_t r = 0; r < rows.size(); ++r) { pin[r] = psi + rows[r]; pout[r] = psih + rows[r]; }
   launch(e, int(rows.size()), [&](char* smem) {
-    ocg::body_hessian_rows<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), psi, xih, rows.data(),
-                               int(rows.size()), u, N, dv.data(), f, H, e.stats + 9);
+    ocg::body_apply_dH<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), pin.data(), pout.data(),
+                           int(rows.size()), nr.data(), e.stats + 6);
+  });
+  for (size_t r = 0; r < rows.size(); ++r) ni[rows[r]] = nr[r];
+  launch(e, int(rows.size()), [&](char* smem) {
+    ocg::body_hessian_rows<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), psih, xih, rows.data(),
+                               int(rows.size()), ni.data(), u, N, dv.data(), f, H, e.stats + 9);
   });
 }
 
@@ -239,13 +249,13 @@ extern "C" int emu_decompose(void* h, int R, int C, const double* M, int dir, do
       for (int q = 1; q <= P.Q1; ++q) c.THO[q] = R * C;
     }
     c.sync();
-    for (int i = c.tid; i < R * C; i += NT) c.TH[i] = double2{M[2 * i], M[2 * i + 1]};
+    for (int i = c.tid; i < R * C; i += NT) c.TH[i] = ocg::c2(M[2 * i], M[2 * i + 1]);
     c.sync();
     c.decompose(dir, cutoff, 1 << 30, false, bound.data());
     if (c.tid == 0) {
       kept = c.KEPT[0];
-      for (int i = 0; i < R * kept; ++i) { X[2 * i] = c.X[i].x; X[2 * i + 1] = c.X[i].y; }
-      for (int i = 0; i < kept * C; ++i) { Y[2 * i] = c.Y[i].x; Y[2 * i + 1] = c.Y[i].y; }
+      for (int i = 0; i < R * kept; ++i) { ocg::zc z = c.X[i]; X[2 * i] = z.x; X[2 * i + 1] = z.y; }
+      for (int i = 0; i < kept * C; ++i) { ocg::zc z = c.Y[i]; Y[2 * i] = z.x; Y[2 * i + 1] = z.y; }
     }
     c.sync();
   });
@@ -272,13 +282,13 @@ extern "C" void emu_decompose_multi(void* h, int nb, const int* Rs, const int* C
     }
     c.sync();
     tot = c.THO[P.Q1];
-    for (int i = c.tid; i < tot; i += NT) c.TH[i] = double2{M[2 * i], M[2 * i + 1]};
+    for (int i = c.tid; i < tot; i += NT) c.TH[i] = ocg::c2(M[2 * i], M[2 * i + 1]);
     c.sync();
     c.decompose(dir, cutoff, 1 << 30, false, bound.data());
     if (c.tid == 0) {
       for (int q = 0; q < nb; ++q) kept[q] = c.KEPT[q];
-      for (int i = 0; i < c.XOFF[P.Q1]; ++i) { X[2 * i] = c.X[i].x; X[2 * i + 1] = c.X[i].y; }
-      for (int i = 0; i < c.YOFF[P.Q1]; ++i) { Y[2 * i] = c.Y[i].x; Y[2 * i + 1] = c.Y[i].y; }
+      for (int i = 0; i < c.XOFF[P.Q1]; ++i) { ocg::zc z = c.X[i]; X[2 * i] = z.x; X[2 * i + 1] = z.y; }
+      for (int i = 0; i < c.YOFF[P.Q1]; ++i) { ocg::zc z = c.Y[i]; Y[2 * i] = z.x; Y[2 * i + 1] = z.y; }
     }
     c.sync();
   });
