@@ -117,6 +117,10 @@ int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_
 int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
                      double* alg_flops, long* sweep_steps);
 int ocg_reset_stats(ocg_ctx* ctx);
+/* diagnostic builds (-DOCG_PROFILE) only: shader-clock cycles per engine phase
+ * (32 slots, see engine_device.hpp Chain::pf), summed over workgroups; zeros in
+ * the product build.  reset != 0 clears after reading. */
+int ocg_profile(ocg_ctx* ctx, double* out32, int reset);
 
 #ifdef __cplusplus
 }

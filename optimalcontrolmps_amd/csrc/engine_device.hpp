@@ -80,7 +80,7 @@ struct LdsLayout {
   int A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
   int ncplx;
   // double buffers (offsets in doubles, after the complex region)
-  int LAM, PP, RED, SCAL;
+  int LAM, PP, RED, SCAL, PROF;
   int ndbl;
   // int buffers (offsets in ints, after the double region)
   int DIMS, MD, BOFF, BOFFT, THR, THC, THO, THRO, THCO, NQ, SIDE, GOFF, EOFF, MQ, POFF, KEPT, XOFF, YOFF, RANK,
@@ -111,6 +111,7 @@ __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   l.PP = d; d += P.evcap;
   l.RED = d; d += nt;
   l.SCAL = d; d += 16;
+  l.PROF = d; d += 32;
   l.ndbl = d;
   int i = 0;
   int Q1 = P.Q1, p = P.p;
@@ -158,7 +159,9 @@ struct Chain {
   const OcgParams& P;
   int tid;
   lzp A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
-  LDS double *LAM, *PP, *RED, *SCAL;
+  LDS double *LAM, *PP, *RED, *SCAL, *PROF;
+  unsigned long long pf_last = 0;
+  int pf_cur = 0;
   LDS int *DIMS, *MD, *BOFF, *BOFFT, *THR, *THC, *THO, *THRO, *THCO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT, *XOFF,
       *YOFF, *RANK, *KIDX, *PART, *ROLE, *PAIR, *CDIM, *COLD, *COFF, *ISCAL;
 
@@ -168,7 +171,7 @@ struct Chain {
     A = cb + l.A; TH = cb + l.TH; G = cb + l.G; G2 = cb + l.G2; W = cb + l.W; W2 = cb + l.W2; X = cb + l.X;
     Y = cb + l.Y; CR = cb + l.CR; S = cb + l.S; GT = cb + l.GT; PH = cb + l.PH; ROT = cb + l.ROT;
     LDS double* db = (cb + l.ncplx).p;
-    LAM = db + l.LAM; PP = db + l.PP; RED = db + l.RED; SCAL = db + l.SCAL;
+    LAM = db + l.LAM; PP = db + l.PP; RED = db + l.RED; SCAL = db + l.SCAL; PROF = db + l.PROF;
     LDS int* ib = (LDS int*)(db + l.ndbl);
     DIMS = ib + l.DIMS; MD = ib + l.MD; BOFF = ib + l.BOFF; BOFFT = ib + l.BOFFT; THR = ib + l.THR; THC = ib + l.THC;
     THO = ib + l.THO; THRO = ib + l.THRO; THCO = ib + l.THCO; NQ = ib + l.NQ; SIDE = ib + l.SIDE;
@@ -179,6 +182,23 @@ struct Chain {
   }
 
   __device__ __forceinline__ void sync() { __syncthreads(); }
+  // Diagnostic build only (-DOCG_PROFILE): thread 0 charges the shader-clock
+  // cycles since the previous stamp to the category that was running.
+  // Categories: 0 build_theta 1 apply_gate 2 gram 3 jacobi 4 rank/truncate
+  // 5 factors X/Y 6 scatter 7 gauge write-back 8 overlap 9 phases/norms
+  // 10 load/store 11 apply_dH zip 12 other.
+  __device__ __forceinline__ void pf(int cat) {
+#ifdef OCG_PROFILE
+    if (tid == 0) {
+      unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (pf_last) PROF[pf_cur] += double(t - pf_last);
+      pf_last = t;
+      pf_cur = cat;
+    }
+#else
+    (void)cat;
+#endif
+  }
   __device__ __forceinline__ int d(int b, int q) const { return (q < 0 || q > P.Q) ? 0 : DIMS[b * P.Q1 + q]; }
   __device__ __forceinline__ int bo(int k, int q, int n) const { return BOFF[((k - 1) * P.Q1 + q) * P.p + n]; }
   __device__ __forceinline__ lzp site(int k) { return A + P.site_base[k]; }
@@ -231,6 +251,7 @@ struct Chain {
 
   // ------------------------------------------------------------- I/O
   __device__ OCG_INLINE void load(const int* gdims, const zc* gdata) {
+    pf(10);
     for (int i = tid; i < P.nsq; i += NT) DIMS[i] = gdims[i];
     for (int i = tid; i < P.cap; i += NT) A[i] = gdata[i];
     sync();
@@ -238,6 +259,7 @@ struct Chain {
     sync();
   }
   __device__ OCG_INLINE void store(int* gdims, zc* gdata) {
+    pf(10);
     for (int i = tid; i < P.nsq; i += NT) gdims[i] = DIMS[i];
     for (int k = 1; k <= P.L; ++k) {
       // number of used elements of site k
@@ -254,6 +276,7 @@ struct Chain {
   // Schmidt-rank bound, capped by Maxm) used to clamp numerically-zero
   // directions out of every decomposition (guards the LDS capacities).
   __device__ OCG_INLINE void load_tables(const zc* gf, const zc* gb, const int* md) {
+    for (int i = tid; i < 32; i += NT) PROF[i] = 0.0;
     for (int i = tid; i < P.gtotal; i += NT) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
     for (int i = tid; i < 2 * P.nsq; i += NT) MD[i] = md[i];
   }
@@ -271,6 +294,7 @@ struct Chain {
     return r;
   }
   __device__ OCG_INLINE double site_norm2(int k) {
+    pf(9);
     int n = P.site_cap[k];
     // sum over used blocks only (unused tail may hold stale data)
     double acc = 0;
@@ -290,6 +314,7 @@ struct Chain {
   }
   // multiply site k by a per-physical-index phase table ph[n]
   __device__ OCG_INLINE void site_phase(int k, lzp ph) {
+    pf(9);
     for (int q = 0; q < P.Q1; ++q)
       for (int n = 0; n < P.p; ++n) {
         int o = bo(k, q, n);
@@ -305,6 +330,7 @@ struct Chain {
   // Two-site tensor for bond (i1, i1+1), blocks by middle QN q:
   //   rows (n1, a in bond i1-1 sector q-n1), cols (n2, c in bond i1+1 sector q+n2)
   __device__ OCG_INLINE void build_theta(int i1) {
+    pf(0);
     const int l = i1 - 1, mid = i1, r = i1 + 1, p = P.p;
     if (tid == 0) {
       int off = 0;
@@ -354,6 +380,7 @@ struct Chain {
   // output element (no runtime-indexed private arrays); the result goes to X
   // and the TH/X buffers are swapped.
   __device__ OCG_INLINE void apply_gate(int i1, int forward, int mode, int lonely) {
+    pf(1);
     const int p = P.p;
     lzp gt = GT + (forward ? 0 : P.gtotal);
     lzp UF = PH;
@@ -540,6 +567,7 @@ struct Chain {
   // `bound` = per-sector rank bound of the new bond (MD row, or MDZ row in
   // the dH zip-up); vectors beyond it are numerically zero and dropped.
   __device__ OCG_INLINE void decompose(int dir, double cutoff, int maxm, bool normalize, const LDS int* bound) {
+    pf(2);
     if (tid == 0) {
       int go = 0, eo = 0, po = 0, maxr = 0;
       for (int q = 0; q < P.Q1; ++q) {
@@ -581,7 +609,9 @@ struct Chain {
     sync();
     lzp Gc = G;
     lzp Wc = W;
+    pf(3);
     jacobi(Gc, Wc);
+    pf(4);
     // eigenvalues + global ranking (descending; ties by flat index)
     const int T = ISCAL[I_EVT];
     for (int e = tid; e < T; e += NT) {
@@ -657,6 +687,7 @@ struct Chain {
       KIDX[EOFF[q] + j] = e - EOFF[q];
     }
     sync();
+    pf(5);
     // materialise X (R x k) and Y (k x C) per block
     const double inv = (normalize && SCAL[S_KEPTW] > 1e-32) ? 1.0 / sqrt(SCAL[S_KEPTW]) : 1.0;
     const int xt = XOFF[P.Q1], yt = YOFF[P.Q1];
@@ -707,6 +738,7 @@ struct Chain {
 
   // write X (rows (n1,a)) into site i1 and Y (cols (n2,c)) into site i1+1
   __device__ OCG_INLINE void scatter_two_site(int i1) {
+    pf(6);
     const int r = i1 + 1, p = P.p;
     if (tid == 0) {
       for (int q = 0; q < P.Q1; ++q) DIMS[i1 * P.Q1 + q] = KEPT[q];
@@ -742,6 +774,7 @@ struct Chain {
   //   left (Fromleft grouping): rows (n, a in bond k-1 sector q-n), cols c in bond k sector q
   //   right (Fromright grouping): rows a in bond k-1 sector q, cols (n, c in bond k sector q+n)
   __device__ OCG_INLINE void site_to_theta(int k, bool left) {
+    pf(7);
     const int p = P.p;
     if (tid == 0) {
       int off = 0;
@@ -795,6 +828,7 @@ struct Chain {
     const int p = P.p;
     site_to_theta(k, true);
     decompose(kFromleft, cutoff, maxm, false, MD + k * P.Q1);
+    pf(7);
     // new offsets of site k+1 with new bond-k dims (into BOFFT)
     if (tid == 0) {
       int off = 0;
@@ -854,6 +888,7 @@ struct Chain {
     const int p = P.p;
     site_to_theta(k, false);
     decompose(kFromright, cutoff, maxm, false, MD + (k - 1) * P.Q1);
+    pf(7);
     if (tid == 0) {
       int off = 0;
       for (int ql = 0; ql < P.Q1; ++ql)
@@ -961,6 +996,7 @@ struct Chain {
   // Scratch: G/G2/W/W2 (environments), X (transfer temp), int tables
   // XOFF/YOFF (env offsets), BOFFT (temp offsets), THRO (X block offsets).
   __device__ OCG_INLINE zc overlap(const int* gd, const zc* gx, int with_dH) {
+    pf(8);
     const int p = P.p, Q1 = P.Q1;
     lzp E0 = G;  lzp E1 = G2;
     lzp N0 = W;  lzp N1 = W2;
@@ -1076,6 +1112,7 @@ struct Chain {
   // right-orthonormal with the (unnormalised) centre at site 1.
   // Carry C_q (new bond k-1 x (s, old bond k-1)) lives in CR at COFF[q].
   __device__ OCG_INLINE void apply_dH(bool truncate_sweep = true) {
+    pf(11);
     const int L = P.L, p = P.p, Q1 = P.Q1;
     LDS int* coff = COFF;   // carry offsets   (Q1+1)
     LDS int* cdim = CDIM;   // carry rows   = new dims of bond k-1
@@ -1153,6 +1190,7 @@ struct Chain {
         break;
       }
       decompose(kFromleft, OCG_GAUGE_CUTOFF, 1 << 30, false, MD + P.nsq + k * P.Q1);
+      pf(11);
       if (tid == 0) {
         // new layout of site k: rows = new bond k-1 (cdim), cols = KEPT
         int o2 = 0;

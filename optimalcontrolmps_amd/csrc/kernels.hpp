@@ -52,8 +52,17 @@ __device__ inline void sweep_model(const Chain<T>& c, double& bytes, double& flo
   flops = f;
 }
 
+#ifdef OCG_PROFILE
+__device__ double g_ocg_prof[32];
+#endif
+
 template <int T>
 __device__ inline void flush_stats(const Chain<T>& c, double* stats, double bytes, double flops, double steps) {
+#ifdef OCG_PROFILE
+  const_cast<Chain<T>&>(c).pf(12);
+  if (threadIdx.x == 0)
+    for (int i = 0; i < 32; ++i) atomicAdd(&g_ocg_prof[i], c.PROF[i]);
+#endif
   if (threadIdx.x == 0 && stats) {
     atomicAdd(stats + 0, bytes);
     atomicAdd(stats + 1, flops);

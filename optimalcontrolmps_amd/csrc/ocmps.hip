@@ -657,6 +657,23 @@ int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, dou
   return 0;
 }
 
+// diagnostic: per-phase shader-clock cycles summed over workgroups (only in
+// a -DOCG_PROFILE build; zeros otherwise).  reset != 0 clears afterwards.
+int ocg_profile(ocg_ctx* c, double* out32, int reset) {
+  if (!c || !out32) return OCG_EINVAL;
+#ifdef OCG_PROFILE
+  HIPCHK(c, hipMemcpyFromSymbol(out32, HIP_SYMBOL(ocg::g_ocg_prof), sizeof(double) * 32));
+  if (reset) {
+    std::vector<double> z(32, 0.0);
+    HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(ocg::g_ocg_prof), z.data(), sizeof(double) * 32));
+  }
+#else
+  (void)reset;
+  for (int i = 0; i < 32; ++i) out32[i] = 0.0;
+#endif
+  return 0;
+}
+
 int ocg_reset_stats(ocg_ctx* c) {
   if (!c) return OCG_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));

@@ -16,7 +16,7 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 LIB_NAME = "liboptimalcontrolmps_amd.so"
-LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+LIB_PATH = os.environ.get("OCG_LIB", os.path.join(PKG_DIR, LIB_NAME))
 CSRC = os.path.join(PKG_DIR, "csrc")
 HEADER = os.path.join(ROOT, "include", "ocmps.h")
 
@@ -84,6 +84,7 @@ SIGNATURES = [
     ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_kernel_stats", C.c_int, [C.c_void_p, C.c_int, dp, C.POINTER(C.c_long), dp, dp, C.POINTER(C.c_long)]),
     ("ocg_reset_stats", C.c_int, [C.c_void_p]),
+    ("ocg_profile", C.c_int, [C.c_void_p, dp, C.c_int]),
 ]
 
 
@@ -258,6 +259,11 @@ class Engine:
                                          C.byref(s)), "ocg_kernel_stats")
         return {"ms": ms.value, "launches": n.value, "alg_bytes": b.value, "alg_flops": f.value,
                 "sweep_steps": s.value}
+
+    def profile(self, reset=True):
+        out = np.zeros(32)
+        self._chk(lib().ocg_profile(self.h, out.ctypes.data_as(dp), int(reset)), "ocg_profile")
+        return out
 
     def reset_stats(self):
         self._chk(lib().ocg_reset_stats(self.h), "ocg_reset_stats")

@@ -15,6 +15,7 @@
 
 thread_local emu_dim3 threadIdx, blockIdx;
 thread_local std::barrier<>* emu_bar;
+thread_local uint64_t* emu_xbuf;
 
 constexpr int NT = 64;
 
@@ -42,12 +43,14 @@ static void launch(Emu& e, int grid, const std::function<void(char*)>& body) {
   for (int b = 0; b < grid; ++b) {
     std::vector<ocg::zc> smem((e.lds + 15) / 16 + 1);
     std::barrier<> bar(NT);
+    std::vector<uint64_t> xb(64, 0);
     std::vector<std::thread> th;
     for (int t = 0; t < NT; ++t)
       th.emplace_back([&, t, b]() {
         threadIdx.x = t;
         blockIdx.x = b;
         emu_bar = &bar;
+        emu_xbuf = xb.data();
         body(reinterpret_cast<char*>(smem.data()));
       });
     for (auto& x : th) x.join();

@@ -1,0 +1,36 @@
+"""Diagnostic: per-phase cycle breakdown of the chain engine (OCG_PROFILE build)."""
+import os, sys, subprocess, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+lib = "/tmp/libocg_prof.so"
+subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                       "-DOCG_PROFILE", "-o", lib, os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip")])
+os.environ["OCG_LIB"] = lib
+import numpy as np
+from optimalcontrolmps_amd import ed
+from optimalcontrolmps_amd.native import MPS, Engine
+NAMES = ["build_theta", "apply_gate", "gram", "jacobi", "rank/trunc", "factors", "scatter", "gauge wb", "overlap",
+         "phase/norm", "load/store", "dH zip", "other"]
+L, p, Q, J, dt = 5, 5, 5, 1.0, 0.01
+ini = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, 2.5)[0], L, p, Q))
+tgt = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, 50.0)[0], L, p, Q))
+eng = Engine(L, p, Q, J, dt, 1e-8, 80)
+u = np.random.default_rng(20261015).uniform(2, 10, 201)
+eng.set_states(tgt, ini)
+for what in ["trajectory(2 chains x 200 steps)", "div_t+xi_dH", "hessian_rows(199)"]:
+    eng.profile(True)
+    t0 = time.perf_counter()
+    if what.startswith("traj"):
+        eng.propagate(u, 3)
+    elif what.startswith("div"):
+        d = eng.div_t(); F = eng.overlap_factor(); eng.xi_dH()
+    else:
+        H = eng.hessian_rows(u, list(range(1, 200)), F, d)
+    t1 = time.perf_counter()
+    pr = eng.profile(True)
+    tot = pr[:13].sum()
+    print(f"== {what}: wall {1e3*(t1-t0):.1f} ms, total cycles {tot:.3e}")
+    for i, n in enumerate(NAMES):
+        if pr[i] > 0:
+            print(f"   {n:12s} {pr[i]:.3e} ({100*pr[i]/tot:5.1f}%)")
+print("traj kernel ms:", eng.stats(0)["ms"], " rows ms:", eng.stats(3)["ms"])
