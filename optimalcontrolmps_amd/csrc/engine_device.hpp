@@ -10,12 +10,23 @@
 //
 // Layout of one MPS (HBM slot and LDS copy alike):
 //   dims[b*Q1 + q]  (int)   bond b = 0..L, sector q = left particle count
-//   data            (zc) site k occupies [site_base[k], +site_cap[k]);
+//   data            (zc)    site k occupies [site_base[k], +site_cap[k]);
 //                   inside it blocks (q, n) (rows dims[k-1][q], cols
-//                   dims[k][q+n]) are packed row-major in (q, n) order.
+//                   dims[k][q+n]) are packed row-major in (q, n) order, so
+//                   the used part of a site is the prefix [0, used_k).
+//
+// Execution model: one chain = one workgroup of NT threads (NT a multiple of
+// 64; the product build uses one wave64).  All bookkeeping is wave-parallel:
+// per-sector tables are built by lane q with DPP prefix scans, per-(q, n)
+// segment tables by chunked scans, and element -> block lookups use
+// v_readlane over a register copy of the block prefix table (no serial
+// thread-0 loops, no dependent LDS search chains).  Every wave primitive is
+// reached by all lanes of its wave (uniform trip counts; per-element work is
+// predicated inside).
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <limits.h>
 
 #include "engine.hpp"
 
@@ -34,9 +45,9 @@ struct __attribute__((aligned(16))) zc {
 #define LDS __attribute__((address_space(3)))
 __host__ __device__ __forceinline__ zc c2(double x, double y) { zc r; r.x = x; r.y = y; return r; }
 
-// LDS complex buffers: an address-space-3 double* (32-bit addresses, ds_*
-// instructions) with complex element access through a converting reference
-// (clang does not let struct copy/assign operate through AS3 pointers).
+// LDS complex buffers: an address-space-3 double* with complex element access
+// through a converting reference (clang does not let struct copy/assign
+// operate through AS3 pointers).
 struct lref {
   LDS double* p;
   __device__ __forceinline__ operator zc() const { return c2(p[0], p[1]); }
@@ -54,7 +65,6 @@ struct lzp {
   __device__ __forceinline__ bool operator==(const lzp& o) const { return p == o.p; }
 };
 __device__ __forceinline__ zc cadd(zc a, zc b) { return c2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ zc csub(zc a, zc b) { return c2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ zc cmul(zc a, zc b) {
   return c2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
 }
@@ -74,23 +84,79 @@ __device__ __forceinline__ void cjacc(zc& acc, zc a, zc b) {  // acc += conj(a)*
 }
 __device__ __forceinline__ double cabs2(zc a) { return a.x * a.x + a.y * a.y; }
 
+// ---------------------------------------------------------------- wave64
+__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double rdlane(double v, int l) {
+  long long b = __double_as_longlong(v);
+  unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(unsigned long long)b, l);
+  unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// DPP row_shr:1,2,4,8 then row_bcast:15 / row_bcast:31 (CDNA wave64 scan idiom);
+// lanes without a source read 0.
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp0(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, 0xf, false); }
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp0(double v) {
+  long long b = __double_as_longlong(v);
+  int lo = dpp0<CTRL, RM>((int)(unsigned)(unsigned long long)b);
+  int hi = dpp0<CTRL, RM>((int)(unsigned)((unsigned long long)b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// inclusive prefix sum over the 64 lanes of the wave
+template <class T>
+__device__ __forceinline__ T wscan(T v) {
+  v += dpp0<0x111, 0xf>(v);
+  v += dpp0<0x112, 0xf>(v);
+  v += dpp0<0x114, 0xf>(v);
+  v += dpp0<0x118, 0xf>(v);
+  v += dpp0<0x142, 0xa>(v);
+  v += dpp0<0x143, 0xc>(v);
+  return v;
+}
+// inclusive prefix max (values >= 0)
+__device__ __forceinline__ int wscan_max(int v) {
+  v = max(v, dpp0<0x111, 0xf>(v));
+  v = max(v, dpp0<0x112, 0xf>(v));
+  v = max(v, dpp0<0x114, 0xf>(v));
+  v = max(v, dpp0<0x118, 0xf>(v));
+  v = max(v, dpp0<0x142, 0xa>(v));
+  v = max(v, dpp0<0x143, 0xc>(v));
+  return v;
+}
+__device__ __forceinline__ double wsum(double v) { return rdlane(wscan(v), 63); }
+// exact a / b for 0 <= a < 2^22, b >= 1 (rcp estimate + one correction each way)
+__device__ __forceinline__ int udiv(int a, int b, int& r) {
+  int q = (int)((float)a * __builtin_amdgcn_rcpf((float)b));
+  r = a - q * b;
+  if (r < 0) { --q; r += b; }
+  if (r >= b) { ++q; r -= b; }
+  return q;
+}
+
+typedef int i4 __attribute__((vector_size(16)));
+
 // ---------------------------------------------------------------- LDS map
 struct LdsLayout {
   // complex buffers (offsets in zc units)
   int A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
   int ncplx;
   // double buffers (offsets in doubles, after the complex region)
-  int LAM, PP, RED, SCAL, PROF;
+  int LAM, PP, SH, RED, SCAL, PROF;
   int ndbl;
   // int buffers (offsets in ints, after the double region)
-  int DIMS, MD, BOFF, BOFFT, THR, THC, THO, THRO, THCO, NQ, SIDE, GOFF, EOFF, MQ, POFF, KEPT, XOFF, YOFF, RANK,
-      KIDX, PART, ROLE, PAIR, CDIM, COLD, COFF, ISCAL;
+  int DIMS, DIMX, MD, BOFF, BOFFT, TRO, TCO, THR, THC, THO, NQ, SIDE, GOFF, EOFF, MQ, POFF, KEPT, XOFF, YOFF, QST,
+      CDIM, COLD, COFF, EQ, RANK, JB, KIDX, ISCAL;
   int nint;
   int bytes;
 };
 
 __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   LdsLayout l;
+  const int Q1 = P.Q1, SEG1 = Q1 * P.p + 1;
+  // per-sector tables: Q1+1 entries padded to a multiple of 8 (b128 searches)
+  const int Q1P = (Q1 + 1 + 7) & ~7;
+  auto al = [](int x) { return (x + 3) & ~3; };  // 16-byte aligned int offsets
   int c = 0;
   l.A = c; c += P.cap;
   l.TH = c; c += P.thcap;
@@ -109,38 +175,39 @@ __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   int d = 0;
   l.LAM = d; d += P.evcap;
   l.PP = d; d += P.evcap;
-  l.RED = d; d += nt;
+  l.SH = d; d += P.nrot + 1;
+  l.RED = d; d += nt / 64 + 1;
   l.SCAL = d; d += 16;
   l.PROF = d; d += 32;
-  l.ndbl = d;
+  l.ndbl = (d + 1) & ~1;
   int i = 0;
-  int Q1 = P.Q1, p = P.p;
-  l.DIMS = i; i += P.nsq;
-  l.MD = i; i += 2 * P.nsq;
-  l.BOFF = i; i += P.L * Q1 * p;
-  l.BOFFT = i; i += Q1 * p;
-  l.THR = i; i += Q1;
-  l.THC = i; i += Q1;
-  l.THO = i; i += Q1 + 1;
-  l.THRO = i; i += Q1 * p;
-  l.THCO = i; i += Q1 * p;
-  l.NQ = i; i += Q1;
-  l.SIDE = i; i += Q1;
-  l.GOFF = i; i += Q1 + 1;
-  l.EOFF = i; i += Q1 + 1;
-  l.MQ = i; i += Q1;
-  l.POFF = i; i += Q1 + 1;
-  l.KEPT = i; i += Q1;
-  l.XOFF = i; i += Q1 + 1;
-  l.YOFF = i; i += Q1 + 1;
-  l.RANK = i; i += P.evcap;
-  l.KIDX = i; i += P.evcap;
-  l.PART = i; i += P.evcap;
-  l.ROLE = i; i += P.evcap;
-  l.PAIR = i; i += P.evcap;
-  l.CDIM = i; i += Q1 + 1;
-  l.COLD = i; i += Q1 + 1;
-  l.COFF = i; i += Q1 + 1;
+  l.DIMS = i; i = al(i + P.nsq);
+  l.DIMX = i; i = al(i + P.nsq);
+  l.MD = i; i = al(i + 2 * P.nsq);
+  l.BOFF = i; i = al(i + P.L * SEG1);
+  l.BOFFT = i; i = al(i + SEG1);
+  l.TRO = i; i = al(i + SEG1);
+  l.TCO = i; i = al(i + SEG1);
+  l.THR = i; i += Q1P;
+  l.THC = i; i += Q1P;
+  l.THO = i; i += Q1P;
+  l.NQ = i; i += Q1P;
+  l.SIDE = i; i += Q1P;
+  l.GOFF = i; i += Q1P;
+  l.EOFF = i; i += Q1P;
+  l.MQ = i; i += Q1P;
+  l.POFF = i; i += Q1P;
+  l.KEPT = i; i += Q1P;
+  l.XOFF = i; i += Q1P;
+  l.YOFF = i; i += Q1P;
+  l.QST = i; i += Q1P;
+  l.CDIM = i; i += Q1P;
+  l.COLD = i; i += Q1P;
+  l.COFF = i; i += Q1P;
+  l.EQ = i; i = al(i + P.evcap);
+  l.RANK = i; i = al(i + P.evcap);
+  l.JB = i; i = al(i + P.evcap);
+  l.KIDX = i; i = al(i + P.evcap);
   l.ISCAL = i; i += 16;
   l.nint = i;
   l.bytes = l.ncplx * 16 + l.ndbl * 8 + l.nint * 4;
@@ -150,34 +217,39 @@ __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
 enum { kFromleft = 0, kFromright = 1 };
 
 // scalar slots
-enum { S_TOTAL = 0, S_KEPTW = 1, S_NORM = 2, S_OVRE = 3, S_OVIM = 4, S_FACT = 5 };
-enum { I_M = 0, I_MAXROUNDS = 1, I_FLAG0 = 2, I_FLAG1 = 3, I_NBLK = 4, I_EVT = 5, I_XT = 6, I_YT = 7, I_THT = 8,
-       I_NPAIR = 9 };
+enum { S_TOTAL = 0, S_KEPTW = 1 };
+enum { I_M = 0, I_MAXROUNDS = 1, I_FLAG = 2 /* ..4 */, I_THT = 8 };
 
 template <int NT>
 struct Chain {
+  static_assert(NT % 64 == 0 && NT <= 1024, "a chain is a whole number of wave64s");
+  static constexpr int NW = NT / 64;
   const OcgParams& P;
-  int tid;
+  const int tid, lane, SEG;
+  const bool w0;
   lzp A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
-  LDS double *LAM, *PP, *RED, *SCAL, *PROF;
+  LDS double *LAM, *PP, *SH, *RED, *SCAL, *PROF;
+  LDS int *DIMS, *DIMX, *MD, *BOFF, *BOFFT, *TRO, *TCO, *THR, *THC, *THO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT,
+      *XOFF, *YOFF, *QST, *CDIM, *COLD, *COFF, *EQ, *RANK, *JB, *KIDX, *ISCAL;
   unsigned long long pf_last = 0;
   int pf_cur = 0;
-  LDS int *DIMS, *MD, *BOFF, *BOFFT, *THR, *THC, *THO, *THRO, *THCO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT, *XOFF,
-      *YOFF, *RANK, *KIDX, *PART, *ROLE, *PAIR, *CDIM, *COLD, *COFF, *ISCAL;
+  // algorithmic-traffic model accumulators (per lane, summed at the end)
+  double m_bytes = 0, m_flops = 0;
 
-  __device__ Chain(const OcgParams& P_, char* smem) : P(P_), tid(threadIdx.x) {
+  __device__ Chain(const OcgParams& P_, char* smem)
+      : P(P_), tid(threadIdx.x), lane(threadIdx.x & 63), SEG(P_.Q1 * P_.p), w0(threadIdx.x < 64) {
     LdsLayout l = lds_layout(P, NT);
     lzp cb{(LDS double*)smem};
     A = cb + l.A; TH = cb + l.TH; G = cb + l.G; G2 = cb + l.G2; W = cb + l.W; W2 = cb + l.W2; X = cb + l.X;
     Y = cb + l.Y; CR = cb + l.CR; S = cb + l.S; GT = cb + l.GT; PH = cb + l.PH; ROT = cb + l.ROT;
     LDS double* db = (cb + l.ncplx).p;
-    LAM = db + l.LAM; PP = db + l.PP; RED = db + l.RED; SCAL = db + l.SCAL; PROF = db + l.PROF;
+    LAM = db + l.LAM; PP = db + l.PP; SH = db + l.SH; RED = db + l.RED; SCAL = db + l.SCAL; PROF = db + l.PROF;
     LDS int* ib = (LDS int*)(db + l.ndbl);
-    DIMS = ib + l.DIMS; MD = ib + l.MD; BOFF = ib + l.BOFF; BOFFT = ib + l.BOFFT; THR = ib + l.THR; THC = ib + l.THC;
-    THO = ib + l.THO; THRO = ib + l.THRO; THCO = ib + l.THCO; NQ = ib + l.NQ; SIDE = ib + l.SIDE;
-    GOFF = ib + l.GOFF; EOFF = ib + l.EOFF; MQ = ib + l.MQ; POFF = ib + l.POFF; KEPT = ib + l.KEPT;
-    XOFF = ib + l.XOFF; YOFF = ib + l.YOFF; RANK = ib + l.RANK; KIDX = ib + l.KIDX; PART = ib + l.PART;
-    ROLE = ib + l.ROLE; PAIR = ib + l.PAIR; CDIM = ib + l.CDIM; COLD = ib + l.COLD; COFF = ib + l.COFF;
+    DIMS = ib + l.DIMS; DIMX = ib + l.DIMX; MD = ib + l.MD; BOFF = ib + l.BOFF; BOFFT = ib + l.BOFFT;
+    TRO = ib + l.TRO; TCO = ib + l.TCO; THR = ib + l.THR; THC = ib + l.THC; THO = ib + l.THO; NQ = ib + l.NQ;
+    SIDE = ib + l.SIDE; GOFF = ib + l.GOFF; EOFF = ib + l.EOFF; MQ = ib + l.MQ; POFF = ib + l.POFF;
+    KEPT = ib + l.KEPT; XOFF = ib + l.XOFF; YOFF = ib + l.YOFF; QST = ib + l.QST; EQ = ib + l.EQ; RANK = ib + l.RANK;
+    JB = ib + l.JB; KIDX = ib + l.KIDX; CDIM = ib + l.CDIM; COLD = ib + l.COLD; COFF = ib + l.COFF;
     ISCAL = ib + l.ISCAL;
   }
 
@@ -200,77 +272,154 @@ struct Chain {
 #endif
   }
   __device__ __forceinline__ int d(int b, int q) const { return (q < 0 || q > P.Q) ? 0 : DIMS[b * P.Q1 + q]; }
-  __device__ __forceinline__ int bo(int k, int q, int n) const { return BOFF[((k - 1) * P.Q1 + q) * P.p + n]; }
+  __device__ __forceinline__ int dx(int b, int q) const { return (q < 0 || q > P.Q) ? 0 : DIMX[b * P.Q1 + q]; }
+  // per-site monotone block-offset table: [q*p + n] = start of block (q, n)
+  // (empty blocks have zero length), [SEG] = used elements of the site
+  __device__ __forceinline__ LDS int* boff(int k) const { return BOFF + (k - 1) * (SEG + 1); }
+  __device__ __forceinline__ int bo(int k, int q, int n) const { return boff(k)[q * P.p + n]; }
+  __device__ __forceinline__ int site_used(int k) const { return boff(k)[SEG]; }
   __device__ __forceinline__ lzp site(int k) { return A + P.site_base[k]; }
 
-  // ------------------------------------------------------------- tables
-  // block offsets of site k from the current dims (single thread)
-  __device__ OCG_INLINE int site_offsets_serial(int k, LDS int* out) const {
-    int off = 0;
-    for (int q = 0; q < P.Q1; ++q)
-      for (int n = 0; n < P.p; ++n) {
-        int r = d(k - 1, q), c = (q + n <= P.Q) ? d(k, q + n) : 0;
-        if (r > 0 && c > 0) { out[q * P.p + n] = off; off += r * c; }
-        else out[q * P.p + n] = -1;
-      }
-    return off;
-  }
-  __device__ OCG_INLINE void all_offsets() {  // parallel over sites
-    for (int k = 1 + tid; k <= P.L; k += NT) site_offsets_serial(k, BOFF + (k - 1) * P.Q1 * P.p);
-  }
-  // (q, local) of the idx-th state of bond b
-  __device__ __forceinline__ void bond_split(int b, int idx, int& q, int& loc) const {
-    int acc = 0;
-    for (q = 0; q < P.Q1; ++q) {
-      int dq = DIMS[b * P.Q1 + q];
-      if (idx < acc + dq) { loc = idx - acc; return; }
-      acc += dq;
+  // ------------------------------------------------------------- wave tables
+  // block of element e in a per-sector prefix table T (Q1 starts, padded to a
+  // multiple of 8, 16-byte aligned): last q with T[q] <= e.  Empty blocks
+  // share the next block's start, so the last match is never empty.  Two
+  // b128 broadcast loads per 8 sectors (one LDS round trip for Q1 <= 8).
+  __device__ __forceinline__ int blk(const LDS int* T, int e) const {
+    const int Q1 = P.Q1;
+    int q = -1;
+    for (int c = 0; c < Q1; c += 8) {
+      const i4 a = *(const LDS i4*)(T + c);
+      const i4 b = *(const LDS i4*)(T + c + 4);
+      q += (a[0] <= e) + (c + 1 < Q1 && a[1] <= e) + (c + 2 < Q1 && a[2] <= e) + (c + 3 < Q1 && a[3] <= e) +
+           (c + 4 < Q1 && b[0] <= e) + (c + 5 < Q1 && b[1] <= e) + (c + 6 < Q1 && b[2] <= e) +
+           (c + 7 < Q1 && b[3] <= e);
     }
-    q = -1; loc = -1;
+    return q;
   }
-  __device__ __forceinline__ int bond_dim(int b) const {
-    int s = 0;
-    for (int q = 0; q < P.Q1; ++q) s += DIMS[b * P.Q1 + q];
+  // segment n of block q in a (q, n)-ordered prefix table TO containing
+  // within-block offset x; o = offset of that segment relative to the block
+  __device__ __forceinline__ int seg_in(const LDS int* TO, int q, int x, int& o) const {
+    const int base = q * P.p, b0 = TO[base], lim = b0 + x;
+    int n = 0, on = b0;
+#pragma unroll
+    for (int t = 1; t < OCG_MAXP; ++t)
+      if (t < P.p) {
+        int v = TO[base + t];
+        if (v <= lim) { n = t; on = v; }
+      }
+    o = on - b0;
+    return n;
+  }
+  // per-q starts of a (q, n) table into QST (one wave; caller syncs)
+  __device__ __forceinline__ void qstarts(const LDS int* B) {
+    if (lane < P.Q1) QST[lane] = B[lane * P.p];
+  }
+  // (q, n, start) of element e of a site laid out by the (q, n) table B
+  // (QST must hold B's per-q starts)
+  __device__ __forceinline__ void find_qn(const LDS int* B, int e, int& q, int& n, int& o) const {
+    q = blk(QST, e);
+    const int base = q * P.p;
+    n = 0;
+    o = B[base];
+#pragma unroll
+    for (int t = 1; t < OCG_MAXP; ++t)
+      if (t < P.p) {
+        int v = B[base + t];
+        if (v <= e) { n = t; o = v; }
+      }
+  }
+  // chunked exclusive scan over [0, n) by one wave: out[i] = sum_{j<i} len(j), out[n] = total
+  // (if qs: qs[q] = out[q*p], the per-q starts of a (q, n) table)
+  template <class F>
+  __device__ OCG_INLINE int scan_excl(LDS int* out, int n, F len, LDS int* qs = nullptr) const {
+    int carry = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      const int v = i < n ? len(i) : 0;
+      const int inc = wscan(v);
+      if (i < n) {
+        out[i] = carry + inc - v;
+        if (qs) {
+          int q, nn;
+          q = udiv(i, P.p, nn);
+          if (nn == 0) qs[q] = carry + inc - v;
+        }
+      }
+      carry += rdlane(inc, 63);
+    }
+    if (lane == 0) out[n] = carry;
+    return carry;
+  }
+  // (q, n) of a flat segment index s = q*p + n
+  __device__ __forceinline__ void qn_of(int s, int& q, int& n) const { q = udiv(s, P.p, n); }
+  // block offsets of site k from the current dims (one wave)
+  __device__ OCG_INLINE void site_offsets(int k) {
+    scan_excl(boff(k), SEG, [&](int s) {
+      int q, n;
+      qn_of(s, q, n);
+      return d(k - 1, q) * d(k, q + n);
+    });
+  }
+  __device__ OCG_INLINE double block_sum(double v) {
+    double w = wsum(v);
+    if (NW == 1) return w;
+    if (lane == 0) RED[tid >> 6] = w;
+    sync();
+    double s = 0;
+    for (int i = 0; i < NW; ++i) s += RED[i];
+    sync();
     return s;
   }
-  // segment lookup in a (Q1 x p) offset table: find n with off[n] <= r < off[n] + len(n)
-  __device__ __forceinline__ int seg_find(const LDS int* offs, int r) const {
-    int best = -1, bo = -1;
-    for (int n = 0; n < P.p; ++n) {
-      int o = offs[n];
-      if (o >= 0 && o <= r && o > bo) { bo = o; best = n; }
+  // per-sector Θ tables from row-segment and column-segment lengths:
+  // TRO/TCO (q, n) prefix tables, THR/THC block shapes (0 if empty), THO
+  // block starts; returns the element count.  Uniform.
+  template <class FR, class FC>
+  __device__ OCG_INLINE int theta_tables(FR rowlen, FC collen) {
+    if (w0) {
+      scan_excl(TRO, SEG, [&](int s) { int q, n; qn_of(s, q, n); return rowlen(q, n); });
+      scan_excl(TCO, SEG, [&](int s) { int q, n; qn_of(s, q, n); return collen(q, n); });
     }
-    return best;
-  }
-  // flat element -> block q using prefix table off[0..Q1]
-  __device__ __forceinline__ int blk_find(const LDS int* off, int e) const {
-    int q = 0;
-    while (q + 1 < P.Q1 && off[q + 1] <= e) ++q;
-    return q;
+    sync();
+    if (w0) {
+      const int q = lane;
+      int R = 0, C = 0;
+      if (q < P.Q1) { R = TRO[(q + 1) * P.p] - TRO[q * P.p]; C = TCO[(q + 1) * P.p] - TCO[q * P.p]; }
+      if (R == 0 || C == 0) { R = 0; C = 0; }
+      const int inc = wscan(R * C);
+      if (q < P.Q1) { THR[q] = R; THC[q] = C; THO[q] = inc - R * C; }
+      if (lane == 63) { THO[P.Q1] = inc; ISCAL[I_THT] = inc; }  // lane 63 holds the total
+    }
+    sync();
+    return ISCAL[I_THT];
   }
 
   // ------------------------------------------------------------- I/O
   __device__ OCG_INLINE void load(const int* gdims, const zc* gdata) {
     pf(10);
     for (int i = tid; i < P.nsq; i += NT) DIMS[i] = gdims[i];
-    for (int i = tid; i < P.cap; i += NT) A[i] = gdata[i];
     sync();
-    all_offsets();
+    for (int k = 1 + (tid >> 6); k <= P.L; k += NW) site_offsets(k);
+    sync();
+    for (int k = 1; k <= P.L; ++k) {
+      const int n = site_used(k), b = P.site_base[k];
+      int i = tid;
+      for (; i + 3 * NT < n; i += 4 * NT) {
+        zc v0 = gdata[b + i], v1 = gdata[b + i + NT], v2 = gdata[b + i + 2 * NT], v3 = gdata[b + i + 3 * NT];
+        A[b + i] = v0; A[b + i + NT] = v1; A[b + i + 2 * NT] = v2; A[b + i + 3 * NT] = v3;
+      }
+      for (; i < n; i += NT) A[b + i] = gdata[b + i];
+    }
     sync();
   }
   __device__ OCG_INLINE void store(int* gdims, zc* gdata) {
     pf(10);
     for (int i = tid; i < P.nsq; i += NT) gdims[i] = DIMS[i];
     for (int k = 1; k <= P.L; ++k) {
-      // number of used elements of site k
-      int last = 0;
-      for (int q = 0; q < P.Q1; ++q)
-        for (int n = 0; n < P.p; ++n) {
-          int o = bo(k, q, n);
-          if (o >= 0) { int e = o + d(k - 1, q) * d(k, q + n); if (e > last) last = e; }
-        }
-      for (int i = tid; i < last; i += NT) gdata[P.site_base[k] + i] = A[P.site_base[k] + i];
+      const int n = site_used(k), b = P.site_base[k];
+      for (int i = tid; i < n; i += NT) gdata[b + i] = A[b + i];
     }
+    sync();
   }
   // gate tables and the per-sector rank bound md[b][q] (Hilbert-space
   // Schmidt-rank bound, capped by Maxm) used to clamp numerically-zero
@@ -280,49 +429,42 @@ struct Chain {
     for (int i = tid; i < P.gtotal; i += NT) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
     for (int i = tid; i < 2 * P.nsq; i += NT) MD[i] = md[i];
   }
+  // traffic-model totals (valid in thread 0; uniform call)
+  __device__ OCG_INLINE void model_totals(double& b, double& f) const {
+    b = wsum(m_bytes);
+    f = wsum(m_flops);
+  }
+  // complex elements of the current MPS (uniform)
+  __device__ OCG_INLINE double mps_used() const {
+    double v = (lane >= 1 && lane <= P.L) ? double(site_used(lane)) : 0.0;
+    return wsum(v);
+  }
 
   // ------------------------------------------------------------- norms
-  __device__ OCG_INLINE double block_reduce_sum(double v) {
-    RED[tid] = v;
-    sync();
-    for (int s = NT / 2; s > 0; s >>= 1) {
-      if (tid < s) RED[tid] += RED[tid + s];
-      sync();
-    }
-    double r = RED[0];
-    sync();
-    return r;
-  }
   __device__ OCG_INLINE double site_norm2(int k) {
     pf(9);
-    int n = P.site_cap[k];
-    // sum over used blocks only (unused tail may hold stale data)
+    const int n = site_used(k);
     double acc = 0;
-    for (int q = 0; q < P.Q1; ++q)
-      for (int nn = 0; nn < P.p; ++nn) {
-        int o = bo(k, q, nn);
-        if (o < 0) continue;
-        int sz = d(k - 1, q) * d(k, q + nn);
-        for (int i = tid; i < sz; i += NT) acc += cabs2(site(k)[o + i]);
-      }
-    (void)n;
-    return block_reduce_sum(acc);
+    for (int i = tid; i < n; i += NT) acc += cabs2(site(k)[i]);
+    return block_sum(acc);
   }
   __device__ OCG_INLINE void site_scale(int k, double f) {
-    for (int i = tid; i < P.site_cap[k]; i += NT) site(k)[i] = cscale(site(k)[i], f);
+    const int n = site_used(k);
+    for (int i = tid; i < n; i += NT) site(k)[i] = cscale(site(k)[i], f);
     sync();
   }
   // multiply site k by a per-physical-index phase table ph[n]
   __device__ OCG_INLINE void site_phase(int k, lzp ph) {
     pf(9);
-    for (int q = 0; q < P.Q1; ++q)
-      for (int n = 0; n < P.p; ++n) {
-        int o = bo(k, q, n);
-        if (o < 0) continue;
-        int sz = d(k - 1, q) * d(k, q + n);
-        zc f = ph[n];
-        for (int i = tid; i < sz; i += NT) site(k)[o + i] = cmul(site(k)[o + i], f);
-      }
+    const LDS int* B = boff(k);
+    if (w0) qstarts(B);
+    sync();
+    const int tot = B[SEG];
+    for (int e = tid; e < tot; e += NT) {
+      int q, n, o;
+      find_qn(B, e, q, n, o);
+      site(k)[e] = cmul(site(k)[e], ph[n]);
+    }
     sync();
   }
 
@@ -331,45 +473,39 @@ struct Chain {
   //   rows (n1, a in bond i1-1 sector q-n1), cols (n2, c in bond i1+1 sector q+n2)
   __device__ OCG_INLINE void build_theta(int i1) {
     pf(0);
-    const int l = i1 - 1, mid = i1, r = i1 + 1, p = P.p;
-    if (tid == 0) {
-      int off = 0;
-      for (int q = 0; q < P.Q1; ++q) {
-        int R = 0, C = 0;
-        for (int n1 = 0; n1 < p; ++n1) {
-          int dl = d(l, q - n1);
-          THRO[q * p + n1] = dl > 0 ? R : -1;
-          R += dl;
-        }
-        for (int n2 = 0; n2 < p; ++n2) {
-          int dr = (q + n2 <= P.Q) ? d(r, q + n2) : 0;
-          THCO[q * p + n2] = dr > 0 ? C : -1;
-          C += dr;
-        }
-        if (R == 0 || C == 0) { R = 0; C = 0; }
-        THR[q] = R; THC[q] = C; THO[q] = off;
-        off += R * C;
+    const int l = i1 - 1, mid = i1, r = i1 + 1;
+    pf(15);
+    const int tot = theta_tables([&](int q, int n) { return d(l, q - n); },
+                                 [&](int q, int n) { return d(r, q + n); });
+    pf(0);
+        // traffic model of this two-site update
+    if (w0) {
+      if (lane < P.Q1) {
+        const double R = THR[lane], C = THC[lane], m = d(mid, lane), n = R < C ? R : C;
+        m_flops += 8.0 * (R * C * m + R * C * P.p + n * n * (R > C ? R : C) + 2.0 * R * C * m);
       }
-      THO[P.Q1] = off;
-      ISCAL[I_THT] = off;
+      if (lane == 0) m_bytes += 16.0 * (2.0 * (site_used(i1) + site_used(r)) + P.gtotal);
     }
-    sync();
-    const int tot = ISCAL[I_THT];
-    for (int e = tid; e < tot; e += NT) {
-      int q = blk_find(THO, e);
-      int loc = e - THO[q], C = THC[q];
-      int row = loc / C, col = loc - row * C;
-      int n1 = seg_find(THRO + q * p, row), n2 = seg_find(THCO + q * p, col);
-      int ia = row - THRO[q * p + n1], ic = col - THCO[q * p + n2];
-      int dm = d(mid, q);
-      zc acc = c2(0, 0);
-      if (dm > 0) {
-        lzp X1 = site(i1) + bo(i1, q - n1, n1) + ia * dm;
-        int drc = d(r, q + n2);
-        lzp X2 = site(r) + bo(r, q, n2) + ic;
-        for (int b = 0; b < dm; ++b) cacc(acc, X1[b], X2[b * drc]);
+    for (int base = 0; base < tot; base += NT) {
+      const int e = base + tid;
+      const int q = blk(THO, e);
+      if (e < tot) {
+        const int C = THC[q];
+        int col;
+        const int row = udiv(e - THO[q], C, col);
+        int o1, o2;
+        const int n1 = seg_in(TRO, q, row, o1), n2 = seg_in(TCO, q, col, o2);
+        const int ia = row - o1, ic = col - o2;
+        const int dm = d(mid, q);
+        zc acc = c2(0, 0);
+        if (dm > 0) {
+          lzp X1 = site(i1) + bo(i1, q - n1, n1) + ia * dm;
+          const int drc = d(r, q + n2);
+          lzp X2 = site(r) + bo(r, q, n2) + ic;
+          for (int b = 0; b < dm; ++b) cacc(acc, X1[b], X2[b * drc]);
+        }
+        TH[e] = acc;
       }
-      TH[e] = acc;
     }
     sync();
   }
@@ -377,8 +513,7 @@ struct Chain {
   // pre-phase -> hopping gate (per Δ = n1+n2 block) -> post-phase, on every
   // (a, c) vector of Θ.  mode 0: left-moving (UF both, optional lonely UT on
   // n2); mode 1: right-moving (UT both after the gate).  One thread per
-  // output element (no runtime-indexed private arrays); the result goes to X
-  // and the TH/X buffers are swapped.
+  // output element; the result goes to X and the TH/X buffers are swapped.
   __device__ OCG_INLINE void apply_gate(int i1, int forward, int mode, int lonely) {
     pf(1);
     const int p = P.p;
@@ -386,175 +521,229 @@ struct Chain {
     lzp UF = PH;
     lzp UT = PH + p;
     const int tot = ISCAL[I_THT];
-    for (int e = tid; e < tot; e += NT) {
-      int q = blk_find(THO, e);
-      int loc = e - THO[q], C = THC[q];
-      int row = loc / C, col = loc - row * C;
-      int a1 = seg_find(THRO + q * p, row), a2 = seg_find(THCO + q * p, col);
-      int ia = row - THRO[q * p + a1], ic = col - THCO[q * p + a2];
-      int D = a1 + a2, ql = q - a1;
-      int lo = P.glo[D], sz = P.gsz[D], y = a1 - lo;
-      lzp g = gt + P.goff[D] + y * sz;
-      zc acc = c2(0, 0);
-      for (int x = 0; x < sz; ++x) {
-        int n1 = lo + x, n2 = D - n1, qs = ql + n1;
-        zc z = TH[THO[qs] + (THRO[qs * p + n1] + ia) * THC[qs] + THCO[qs * p + n2] + ic];
-        if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
-        cacc(acc, g[x], z);
+        for (int base = 0; base < tot; base += NT) {
+      const int e = base + tid;
+      const int q = blk(THO, e);
+      if (e < tot) {
+        const int C = THC[q];
+        int col;
+        const int row = udiv(e - THO[q], C, col);
+        int o1, o2;
+        const int a1 = seg_in(TRO, q, row, o1), a2 = seg_in(TCO, q, col, o2);
+        const int ia = row - o1, ic = col - o2;
+        const int D = a1 + a2, ql = q - a1;
+        const int lo = P.glo[D], sz = P.gsz[D], y = a1 - lo;
+        lzp g = gt + P.goff[D] + y * sz;
+        zc acc = c2(0, 0);
+        for (int x = 0; x < sz; ++x) {
+          const int n1 = lo + x, n2 = D - n1, qs = ql + n1;
+          const int ro = TRO[qs * p + n1] - TRO[qs * p], co = TCO[qs * p + n2] - TCO[qs * p];
+          zc z = TH[THO[qs] + (ro + ia) * THC[qs] + co + ic];
+          if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
+          cacc(acc, g[x], z);
+        }
+        if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
+        else if (lonely) acc = cmul(acc, UT[a2]);
+        X[e] = acc;
       }
-      if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
-      else if (lonely) acc = cmul(acc, UT[a2]);
-      X[e] = acc;
     }
     sync();
     lzp t = TH; TH = X; X = t;
   }
 
   // ------------------------------------------------------------- Jacobi
+  // Pairing of index x of a block (m even, M = m-1 rounds) in round r of the
+  // circle method: pair 0 = {r, M}; pair k = {(r+k) mod M, (r-k) mod M}.
+  // Returns the pair id (-1 if x is idle this round) and its partner.
+  __device__ __forceinline__ int jpair(int x, int r, int m, int n, int& px) const {
+    const int M = m - 1;
+    if (r >= M) return -1;
+    int k;
+    if (x == M) { px = r; k = 0; }
+    else if (x == r) { px = M; k = 0; }
+    else {
+      int dd = x - r;
+      if (dd < 0) dd += M;
+      k = (2 * dd <= M) ? dd : M - dd;
+      px = 2 * r - x;
+      if (px < 0) px += M;
+      if (px >= M) px -= M;
+    }
+    return (px < n) ? k : -1;
+  }
+  // coefficients of column x of J for pair (cs = (c, s), e):
+  //   x = p: J[p][p] = c,     J[q][p] = -s e*
+  //   x = q: J[q][q] = c e*,  J[p][q] = s
+  __device__ __forceinline__ void jcol(int x, int px, zc cs, zc e, zc& jd, zc& jo) const {
+    if (x < px) { jd = c2(cs.x, 0); jo = cscale(cconj(e), -cs.y); }
+    else { jd = cscale(cconj(e), cs.x); jo = c2(cs.y, 0); }
+  }
+  // Gram element (i, j) of block q with the block data phase B needs
+  struct JD {
+    int i, j, n, m, go, po;  // n == 0: no element
+  };
+  __device__ __forceinline__ JD jd_of(int e, int nel) const {
+    JD r{0, 0, 0, 0, 0, 0};
+    if (e < nel) {
+      const int q = blk(GOFF, e);
+      r.n = NQ[q]; r.m = MQ[q]; r.go = GOFF[q]; r.po = POFF[q];
+      r.i = udiv(e - r.go, r.n, r.j);
+    }
+    return r;
+  }
+  // rotation pair t = (block q, pair k)
+  struct JP {
+    int k, n, m, go;  // n == 0: no pair
+  };
+  __device__ __forceinline__ JP jp_of(int t, int npair) const {
+    JP r{0, 0, 0, 0};
+    if (t < npair) {
+      const int q = blk(POFF, t);
+      r.k = t - POFF[q]; r.n = NQ[q]; r.m = MQ[q]; r.go = GOFF[q];
+    }
+    return r;
+  }
+  // Phase A: complex Jacobi rotation zeroing g[p][q] of pair t in round rnd.
+  // With D = aqq - app, b = g[p][q], r = |b| (the classical tan formula
+  // t = sgn(D) / (|tau| + sqrt(1 + tau^2)), tau = D / (2 r), cleared of divisions):
+  //   R = sqrt(D^2 + 4 r^2), E = |D| + R, c = E / sqrt(E^2 + 4 r^2),
+  //   s = sgn(D) 2 r / sqrt(E^2 + 4 r^2), shift = sgn(D) 2 r^2 / E, e = b / r.
+  __device__ __forceinline__ void jrot(const JP& d, int t, int rnd, lzp Gc) {
+    if (d.n == 0) return;
+    const int M = d.m - 1, n = d.n;
+    zc cs = c2(1.0, 0.0), e = c2(1.0, 0.0);
+    double shift = 0.0;
+    if (rnd < M) {
+      int a, b;
+      if (d.k == 0) { a = rnd; b = M; }
+      else {
+        a = rnd + d.k; if (a >= M) a -= M;
+        b = rnd - d.k; if (b < 0) b += M;
+      }
+      const int pp_ = a < b ? a : b, qq_ = a < b ? b : a;
+      if (qq_ < n) {
+        lzp g = Gc + d.go;
+        zc bv = g[pp_ * n + qq_];
+        double app = zc(g[pp_ * n + pp_]).x, aqq = zc(g[qq_ * n + qq_]).x;
+        const double sz = fabs(app) + fabs(aqq);
+        const double mb = fmax(fabs(bv.x), fabs(bv.y));
+        // skip rotations whose off-diagonal is below working precision of the diagonal
+        if (mb > 1e-300 && mb > 1e-18 * sz) {
+          // power-of-two rescale keeps r^2 and D^2 in range (exact, rare)
+          double sc = 1.0;
+          if (mb < 1e-120 || mb > 1e120 || sz > 1e120) {
+            sc = ldexp(1.0, -ilogb(fmax(mb, sz)));
+            bv = cscale(bv, sc); app *= sc; aqq *= sc;
+          }
+          const double r2 = bv.x * bv.x + bv.y * bv.y;
+          const double rinv = rsqrt(r2), r = r2 * rinv;
+          const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
+          const double E = fabs(D) + sqrt(fma(D, D, 4.0 * r2));
+          const double h = rsqrt(fma(E, E, 4.0 * r2));
+          cs = c2(E * h, sg * 2.0 * r * h);
+          e = c2(bv.x * rinv, bv.y * rinv);
+          shift = sg * 2.0 * r2 / E / sc;
+        }
+      }
+    }
+    ROT[2 * t] = cs;
+    ROT[2 * t + 1] = e;
+    SH[t] = shift;
+  }
+  // Phase B: G'[i][j] = (J^H G J)[i][j] and W'[i][j] = (W J)[i][j]
+  __device__ __forceinline__ void jupd(const JD& d, int rnd, lzp Gc, lzp Wc, lzp Gn, lzp Wn, bool lastr, int fl) {
+    if (d.n == 0) return;
+    const int i = d.i, j = d.j, n = d.n, m = d.m, loc = i * n + j;
+    lzp gs = Gc + d.go, ws = Wc + d.go;
+    int pj = j, pi = i;
+    const int kj = (m > 0) ? jpair(j, rnd, m, n, pj) : -1;
+    const int ki = (m > 0) ? jpair(i, rnd, m, n, pi) : -1;
+    zc jjj = c2(1, 0), jpj = c2(0, 0), jii = c2(1, 0), jpi = c2(0, 0);
+    bool rotj = false, roti = false;
+    if (kj >= 0) {
+      const zc cs = ROT[2 * (d.po + kj)], ee = ROT[2 * (d.po + kj) + 1];
+      rotj = cs.y != 0.0;
+      jcol(j, pj, cs, ee, jjj, jpj);
+    }
+    if (ki >= 0) {
+      const zc cs = ROT[2 * (d.po + ki)], ee = ROT[2 * (d.po + ki) + 1];
+      roti = cs.y != 0.0;
+      jcol(i, pi, cs, ee, jii, jpi);
+    }
+    // W'[i][j] = W[i][j] J[j][j] + W[i][j'] J[j'][j]
+    zc w = cmul(ws[loc], jjj);
+    if (rotj) cacc(w, ws[i * n + pj], jpj);
+    Wn[d.go + loc] = w;
+    zc out;
+    if (rotj && pi == j && ki >= 0) {
+      out = c2(0, 0);  // the rotated 2x2 block: exact zero off-diagonal
+    } else if (rotj && i == j) {
+      const double sh = SH[d.po + kj];
+      out = c2(zc(gs[loc]).x + (j < pj ? -sh : sh), 0);
+    } else {
+      // sum_{k in {i,i'}} sum_{l in {j,j'}} conj(J[k][i]) G[k][l] J[l][j]
+      zc r0 = cmul(gs[loc], jjj);
+      if (rotj) cacc(r0, gs[i * n + pj], jpj);
+      out = cjmul(jii, r0);
+      if (roti) {
+        zc r1 = cmul(gs[pi * n + j], jjj);
+        if (rotj) cacc(r1, gs[pi * n + pj], jpj);
+        cjacc(out, jpi, r1);
+      }
+    }
+    // convergence: an off-diagonal entry above 1e-15 of its diagonal pair
+    if (lastr && i < j) {
+      const double sz = fabs(zc(gs[i * n + i]).x) + fabs(zc(gs[j * n + j]).x);
+      if (cabs2(out) > 1e-30 * sz * sz) atomicOr((int*)&ISCAL[fl], 1);
+    }
+    Gn[d.go + loc] = out;
+  }
   // Parallel (round-robin) complex Jacobi on all Gram blocks at once.
   // Block q: n = NQ[q] at G + GOFF[q]; eigenvectors accumulated in W.
-  // On exit G/W point at the converged buffers (diag = eigenvalues).
+  // Element/pair descriptors are computed once and kept in registers for
+  // all rounds (JB_IT x NT elements, JA_IT x NT pairs; larger problems fall
+  // back to per-round lookups).  Convergence is tested on the output of each
+  // sweep's last round.  On exit Gc/Wc point at the converged buffers.
   __device__ OCG_INLINE void jacobi(lzp& Gc, lzp& Wc) {
+    constexpr int JB_IT = 4, JA_IT = 2;
     lzp Gn = (Gc == G) ? G2 : G;
     lzp Wn = (Wc == W) ? W2 : W;
     const int maxr = ISCAL[I_MAXROUNDS];
     if (maxr <= 0) return;
-    const int npair = ISCAL[I_NPAIR];
+    const int npair = POFF[P.Q1];
     const int nel = GOFF[P.Q1];
-    for (int sweep = 0; sweep < 40; ++sweep) {
+    JD dB[JB_IT];
+    JP dA[JA_IT];
+#pragma unroll
+    for (int it = 0; it < JB_IT; ++it) dB[it] = jd_of(it * NT + tid, nel);
+#pragma unroll
+    for (int it = 0; it < JA_IT; ++it) dA[it] = jp_of(it * NT + tid, npair);
+    int sweep = 0;
+    for (; sweep < 40; ++sweep) {
+      const int fl = I_FLAG + sweep % 3;
       for (int rnd = 0; rnd < maxr; ++rnd) {
-        // Phase A: rotation parameters for every (block, pair)
-        for (int t = tid; t < npair; t += NT) {
-          int q = blk_find(POFF, t);
-          int k = t - POFF[q], m = MQ[q], n = NQ[q];
-          int pp_, qq_;
-          bool active = rnd < m - 1;
-          if (k == 0) { pp_ = m - 1; qq_ = rnd; }
-          else { pp_ = (rnd + k) % (m - 1); qq_ = (rnd - k + m - 1) % (m - 1); }
-          if (pp_ > qq_) { int tmp = pp_; pp_ = qq_; qq_ = tmp; }
-          zc cs = c2(1.0, 0.0), e = c2(1.0, 0.0);
-          double shift = 0.0;
-          bool rot = false;
-          if (active && qq_ < n) {
-            lzp g = Gc + GOFF[q];
-            zc b = g[pp_ * n + qq_];
-            double ab = hypot(b.x, b.y);  // no underflow: e = b/|b| must stay unit-modulus
-            double app = zc(g[pp_ * n + pp_]).x, aqq = zc(g[qq_ * n + qq_]).x;
-            // skip rotations whose off-diagonal is below working precision of the diagonal
-            if (ab > 1e-300 && ab > 1e-18 * (fabs(app) + fabs(aqq))) {
-              double tau = (aqq - app) / (2.0 * ab);
-              double tt = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-              double c = 1.0 / sqrt(1.0 + tt * tt);
-              cs = c2(c, tt * c);
-              e = c2(b.x / ab, b.y / ab);
-              shift = tt * ab;
-              rot = true;
-            }
-          }
-          ROT[2 * t] = cs;
-          ROT[2 * t + 1] = e;
-          if (active && qq_ < n) {
-            int base = EOFF[q];
-            PART[base + pp_] = qq_; ROLE[base + pp_] = rot ? 0 : 2; PAIR[base + pp_] = t;
-            PART[base + qq_] = pp_; ROLE[base + qq_] = rot ? 1 : 2; PAIR[base + qq_] = t;
-            LAM[base + pp_] = shift;  // reuse LAM as per-index shift scratch
-          } else if (active && pp_ < n) {
-            int base = EOFF[q];
-            ROLE[base + pp_] = 2; PART[base + pp_] = pp_; PAIR[base + pp_] = t;
-          }
-          if (!active) {
-            // block idle this round: all its indices unrotated (written by pair 0 only)
-            if (k == 0) {
-              int base = EOFF[q];
-              for (int i = 0; i < n; ++i) { ROLE[base + i] = 2; PART[base + i] = i; }
-            }
-          }
-        }
+        if (rnd == 0 && tid == 0) ISCAL[I_FLAG + (sweep + 1) % 3] = 0;
+        pf(13);
+#pragma unroll
+        for (int it = 0; it < JA_IT; ++it) jrot(dA[it], it * NT + tid, rnd, Gc);
+        for (int t = JA_IT * NT + tid; t < npair; t += NT) jrot(jp_of(t, npair), t, rnd, Gc);
         sync();
-        // Phase B: G' = J^H G J, W' = W J (double-buffered)
-        for (int t = tid; t < 2 * nel; t += NT) {
-          bool isW = t >= nel;
-          int e = isW ? t - nel : t;
-          int q = blk_find(GOFF, e);
-          int n = NQ[q];
-          int loc = e - GOFF[q];
-          int i = loc / n, j = loc - i * n;
-          int base = EOFF[q];
-          lzp g = (isW ? Wc : Gc) + GOFF[q];
-          if (MQ[q] == 0) {  // 1x1 block: nothing to rotate
-            (isW ? Wn : Gn)[GOFF[q] + loc] = g[loc];
-            continue;
-          }
-          // column-j coefficients of J: J[j][j], J[j'][j]
-          int rj = ROLE[base + j], pj = PART[base + j];
-          zc jjj, jpj;
-          if (rj == 2) { jjj = c2(1, 0); jpj = c2(0, 0); pj = j; }
-          else {
-            zc cs = ROT[2 * PAIR[base + j]], ee = ROT[2 * PAIR[base + j] + 1];
-            if (rj == 0) { jjj = c2(cs.x, 0); jpj = cscale(cconj(ee), -cs.y); }  // J[p][p]=c, J[q][p]=-s e*
-            else { jjj = cscale(cconj(ee), cs.x); jpj = c2(cs.y, 0); }          // J[q][q]=c e*, J[p][q]=s
-          }
-          zc out;
-          if (isW) {
-            // W'[i][j] = W[i][j] J[j][j] + W[i][j'] J[j'][j]
-            out = cmul(g[i * n + j], jjj);
-            if (rj != 2) cacc(out, g[i * n + pj], jpj);
-            Wn[GOFF[q] + loc] = out;
-          } else {
-            int ri = ROLE[base + i], pi = PART[base + i];
-            if (ri != 2 && pi == j) {
-              // the rotated 2x2 block: exact zero off-diagonal
-              out = c2(0, 0);
-            } else if (ri != 2 && i == j) {
-              double sh = LAM[base + (ri == 0 ? i : pi)];
-              out = c2(zc(g[i * n + i]).x + (ri == 0 ? -sh : sh), 0);
-            } else {
-              zc jii, jpi;
-              if (ri == 2) { jii = c2(1, 0); jpi = c2(0, 0); pi = i; }
-              else {
-                zc cs = ROT[2 * PAIR[base + i]], ee = ROT[2 * PAIR[base + i] + 1];
-                if (ri == 0) { jii = c2(cs.x, 0); jpi = cscale(cconj(ee), -cs.y); }
-                else { jii = cscale(cconj(ee), cs.x); jpi = c2(cs.y, 0); }
-              }
-              // sum_{k in {i,i'}} sum_{l in {j,j'}} conj(J[k][i]) G[k][l] J[l][j]
-              zc r0 = cmul(g[i * n + j], jjj);
-              if (rj != 2) cacc(r0, g[i * n + pj], jpj);
-              out = cjmul(jii, r0);
-              if (ri != 2) {
-                zc r1 = cmul(g[pi * n + j], jjj);
-                if (rj != 2) cacc(r1, g[pi * n + pj], jpj);
-                cjacc(out, jpi, r1);
-              }
-            }
-            Gn[GOFF[q] + loc] = out;
-          }
-        }
+        pf(14);
+        const bool lastr = rnd == maxr - 1;
+#pragma unroll
+        for (int it = 0; it < JB_IT; ++it) jupd(dB[it], rnd, Gc, Wc, Gn, Wn, lastr, fl);
+        for (int e = JB_IT * NT + tid; e < nel; e += NT) jupd(jd_of(e, nel), rnd, Gc, Wc, Gn, Wn, lastr, fl);
         sync();
+        pf(3);
         lzp tg = Gc; Gc = Gn; Gn = tg;
         lzp tw = Wc; Wc = Wn; Wn = tw;
       }
-      // convergence check: per block off-diagonal weight vs diagonal weight
-      int fl = (sweep & 1) ? I_FLAG1 : I_FLAG0;
-      int fo = (sweep & 1) ? I_FLAG0 : I_FLAG1;
-      if (tid == 0) ISCAL[fo] = 0;
-      for (int q = tid; q < P.Q1; q += NT) {
-        int n = NQ[q];
-        if (n < 2) continue;
-        lzp g = Gc + GOFF[q];
-        double off = 0, dia = 0;
-        for (int i = 0; i < n; ++i)
-          for (int j = 0; j < n; ++j) {
-            double a = cabs2(g[i * n + j]);
-            if (i == j) dia += a; else off += a;
-          }
-        if (off > 1e-30 * dia) atomicOr((int*)&ISCAL[fl], 1);
-      }
-      sync();
-      int more = ISCAL[fl];
-      sync();
-      if (tid == 0) ISCAL[fl] = 0;
+      const int more = ISCAL[fl];
       if (!more) break;
     }
+#ifdef OCG_PROFILE
+    if (tid == 0) { PROF[20] += sweep + 1; PROF[21] += 1.0; PROF[22] += maxr; }  // sweeps, calls, rounds/sweep
+#endif
   }
 
   // ------------------------------------------------------------- decomposition
@@ -567,44 +756,49 @@ struct Chain {
   // `bound` = per-sector rank bound of the new bond (MD row, or MDZ row in
   // the dH zip-up); vectors beyond it are numerically zero and dropped.
   __device__ OCG_INLINE void decompose(int dir, double cutoff, int maxm, bool normalize, const LDS int* bound) {
-    pf(2);
-    if (tid == 0) {
-      int go = 0, eo = 0, po = 0, maxr = 0;
-      for (int q = 0; q < P.Q1; ++q) {
-        int R = THR[q], C = THC[q];
-        int n = (R == 0 || C == 0) ? 0 : (R <= C ? R : C);
-        NQ[q] = n;
-        SIDE[q] = (R <= C) ? 0 : 1;  // 0: rows side (TH TH^H), 1: cols side (TH^H TH)
-        GOFF[q] = go; go += n * n;
-        EOFF[q] = eo; eo += n;
-        int m = (n >= 2) ? (n + (n & 1)) : 0;
-        MQ[q] = m;
-        POFF[q] = po; po += m / 2;
-        if (m - 1 > maxr) maxr = m - 1;
+    pf(16);
+    const int Q1 = P.Q1;
+    if (w0) {
+      const int q = lane;
+      const int R = q < Q1 ? THR[q] : 0, C = q < Q1 ? THC[q] : 0;
+      const int n = (R == 0 || C == 0) ? 0 : (R <= C ? R : C);
+      const int m = (n >= 2) ? (n + (n & 1)) : 0;
+      const int ig = wscan(n * n), ie = wscan(n), ip = wscan(m / 2), mr = wscan_max(m > 0 ? m - 1 : 0);
+      if (q < Q1) {
+        NQ[q] = n; SIDE[q] = (R <= C) ? 0 : 1;  // 0: rows side (TH TH^H), 1: cols side (TH^H TH)
+        MQ[q] = m; GOFF[q] = ig - n * n; EOFF[q] = ie - n; POFF[q] = ip - m / 2;
+        KEPT[q] = 0;
       }
-      GOFF[P.Q1] = go; EOFF[P.Q1] = eo; POFF[P.Q1] = po;
-      ISCAL[I_MAXROUNDS] = maxr;
-      ISCAL[I_NPAIR] = po;
-      ISCAL[I_EVT] = eo;
-      ISCAL[I_FLAG0] = 0; ISCAL[I_FLAG1] = 0;
+      if (lane == 63) {  // inclusive scans: lane 63 holds the totals
+        GOFF[Q1] = ig; EOFF[Q1] = ie; POFF[Q1] = ip;
+        ISCAL[I_MAXROUNDS] = mr;
+        ISCAL[I_FLAG] = 0; ISCAL[I_FLAG + 1] = 0; ISCAL[I_FLAG + 2] = 0;
+      }
     }
     sync();
+    pf(2);
     // Gram matrices and identity eigenvectors
-    const int nel = GOFF[P.Q1];
-    for (int e = tid; e < nel; e += NT) {
-      int q = blk_find(GOFF, e);
-      int n = NQ[q], loc = e - GOFF[q];
-      int i = loc / n, j = loc - i * n;
-      lzp T = TH + THO[q];
-      int R = THR[q], C = THC[q];
-      zc acc = c2(0, 0);
-      if (SIDE[q] == 0) {
-        for (int c = 0; c < C; ++c) cacc(acc, T[i * C + c], cconj(T[j * C + c]));
-      } else {
-        for (int r = 0; r < R; ++r) cjacc(acc, T[r * C + i], T[r * C + j]);
+    {
+      const int nel = GOFF[Q1];
+      for (int base = 0; base < nel; base += NT) {
+        const int e = base + tid;
+        const int q = blk(GOFF, e);
+        if (e < nel) {
+          const int n = NQ[q];
+          int j;
+          const int i = udiv(e - GOFF[q], n, j);
+          lzp T = TH + THO[q];
+          const int R = THR[q], C = THC[q];
+          zc acc = c2(0, 0);
+          if (SIDE[q] == 0) {
+            for (int c = 0; c < C; ++c) cacc(acc, T[i * C + c], cconj(T[j * C + c]));
+          } else {
+            for (int r = 0; r < R; ++r) cjacc(acc, T[r * C + i], T[r * C + j]);
+          }
+          G[e] = acc;
+          W[e] = (i == j) ? c2(1, 0) : c2(0, 0);
+        }
       }
-      G[e] = acc;
-      W[e] = (i == j) ? c2(1, 0) : c2(0, 0);
     }
     sync();
     lzp Gc = G;
@@ -612,125 +806,143 @@ struct Chain {
     pf(3);
     jacobi(Gc, Wc);
     pf(4);
-    // eigenvalues + global ranking (descending; ties by flat index)
-    const int T = ISCAL[I_EVT];
-    for (int e = tid; e < T; e += NT) {
-      int q = blk_find(EOFF, e);
-      int i = e - EOFF[q], n = NQ[q];
-      double lam = zc(Gc[GOFF[q] + i * n + i]).x;
-      LAM[e] = lam > 0 ? lam : 0.0;
+    // eigenvalues (clamped at 0) and their blocks
+    const int T = EOFF[Q1];
+    {
+      for (int base = 0; base < T; base += NT) {
+        const int e = base + tid;
+        const int q = blk(EOFF, e);
+        if (e < T) {
+          const int i = e - EOFF[q], n = NQ[q];
+          const double lam = zc(Gc[GOFF[q] + i * n + i]).x;
+          LAM[e] = lam > 0 ? lam : 0.0;
+          EQ[e] = q;
+        }
+      }
     }
     sync();
+    // global rank (descending; ties by flat index) and rank within the block
+    // (the competitors are read as LDS broadcasts, four in flight)
     for (int e = tid; e < T; e += NT) {
-      double le = LAM[e];
-      int rk = 0;
-      for (int f = 0; f < T; ++f) {
-        double lf = LAM[f];
-        rk += (lf > le) || (lf == le && f < e);
+      const double le = LAM[e];
+      const int be = EQ[e];
+      int rk = 0, jb = 0;
+      int f = 0;
+      for (; f + 3 < T; f += 4) {
+        const double l0 = LAM[f], l1 = LAM[f + 1], l2 = LAM[f + 2], l3 = LAM[f + 3];
+        const int b0 = EQ[f], b1 = EQ[f + 1], b2 = EQ[f + 2], b3 = EQ[f + 3];
+        const int c0 = (l0 > le) || (l0 == le && f < e), c1 = (l1 > le) || (l1 == le && f + 1 < e);
+        const int c2_ = (l2 > le) || (l2 == le && f + 2 < e), c3 = (l3 > le) || (l3 == le && f + 3 < e);
+        rk += c0 + c1 + c2_ + c3;
+        jb += (c0 & (b0 == be)) + (c1 & (b1 == be)) + (c2_ & (b2 == be)) + (c3 & (b3 == be));
+      }
+      for (; f < T; ++f) {
+        const double lf = LAM[f];
+        const int c = (lf > le) || (lf == le && f < e);
+        rk += c;
+        jb += c & (EQ[f] == be);
       }
       RANK[e] = rk;
+      JB[e] = jb;
       PP[rk] = le;
     }
     sync();
-    // truncation (ITensor truncate; relative cutoff; floor 1e-30)
-    if (tid == 0) {
+    // truncation (ITensor truncate; relative cutoff; floor 1e-30): the
+    // discarded set {j >= 1 : j >= maxm or sum_{i>=j} PP[i] < cutoff*total or
+    // PP[j] <= 1e-30 total} is a suffix of the sorted spectrum
+    if (w0) {
       double total = 0;
-      for (int i = 0; i < T; ++i) total += PP[i];
-      int last = T - 1;
-      double trunc = 0;
-      while (last >= maxm) { trunc += PP[last]; --last; }
-      while (last >= 1 && (trunc + PP[last] < cutoff * total || PP[last] <= 1e-30 * total)) {
-        trunc += PP[last];
-        --last;
+      for (int b = 0; b < T; b += 64) total += wsum((b + lane < T) ? PP[b + lane] : 0.0);
+      const double cut = cutoff * total, floor_ = 1e-30 * total;
+      double carry = 0;
+      int nd = 0;
+      for (int cb = 0; cb < T; cb += 64) {
+        const int j = T - 1 - cb - lane;  // lane 0 = smallest
+        const double v = j >= 0 ? PP[j] : 0.0;
+        const double inc = wscan(v);
+        const double suf = carry + inc;
+        const bool disc = j >= 1 && (j >= maxm || suf < cut || v <= floor_);
+        nd += __popcll(__ballot(disc));
+        carry += rdlane(inc, 63);
       }
-      int m = last + 1;
-      double kw = 0;
-      for (int i = 0; i < m; ++i) kw += PP[i];
-      ISCAL[I_M] = m;
-      SCAL[S_TOTAL] = total;
-      SCAL[S_KEPTW] = kw;
-      // kept per block + output offsets
-      int xo = 0, yo = 0;
-      for (int q = 0; q < P.Q1; ++q) {
-        int k = 0;
-        for (int i = 0; i < NQ[q]; ++i) k += RANK[EOFF[q] + i] < m;
-        int cap = bound[q];
-        if (k > cap) {  // beyond the sector's Schmidt-rank bound: numerical noise
-          for (int r = 0; r < m && k > cap; ++r) {
-            // drop this block's lowest-ranked kept vectors first
-            int worst = -1, wr = -1;
-            for (int i = 0; i < NQ[q]; ++i) {
-              int rk = RANK[EOFF[q] + i];
-              if (rk < m && rk > wr) { wr = rk; worst = i; }
-            }
-            kw -= PP[wr];
-            RANK[EOFF[q] + worst] = 1 << 30;
-            --k;
-          }
-          SCAL[S_KEPTW] = kw;
-        }
-        KEPT[q] = k;
-        XOFF[q] = xo; xo += THR[q] * k;
-        YOFF[q] = yo; yo += k * THC[q];
-      }
-      XOFF[P.Q1] = xo; YOFF[P.Q1] = yo;
+      if (lane == 0) { ISCAL[I_M] = T - nd; SCAL[S_TOTAL] = total; }
     }
-    // kept eigenvector order within each block (by global rank)
     sync();
-    const int m = ISCAL[I_M];
-    for (int e = tid; e < T; e += NT) {
-      int rk = RANK[e];
-      if (rk >= m) continue;
-      int q = blk_find(EOFF, e);
-      int j = 0;
-      for (int f = EOFF[q]; f < EOFF[q + 1]; ++f) j += RANK[f] < rk;
-      KIDX[EOFF[q] + j] = e - EOFF[q];
+    // kept vectors: global rank < m and within the sector's rank bound
+    {
+      const int m = ISCAL[I_M];
+      double kw = 0;
+      for (int e = tid; e < T; e += NT) {
+        const int q = EQ[e], jb = JB[e];
+        if (RANK[e] < m && jb < bound[q]) {
+          atomicAdd((int*)&KEPT[q], 1);
+          KIDX[EOFF[q] + jb] = e - EOFF[q];
+          kw += LAM[e];
+        }
+      }
+      kw = block_sum(kw);
+      if (tid == 0) SCAL[S_KEPTW] = kw;
+    }
+    sync();
+    if (w0) {
+      const int q = lane;
+      const int k = q < Q1 ? KEPT[q] : 0, R = q < Q1 ? THR[q] : 0, C = q < Q1 ? THC[q] : 0;
+      const int ix = wscan(R * k), iy = wscan(k * C);
+      if (q < Q1) { XOFF[q] = ix - R * k; YOFF[q] = iy - k * C; }
+      if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; }
     }
     sync();
     pf(5);
     // materialise X (R x k) and Y (k x C) per block
-    const double inv = (normalize && SCAL[S_KEPTW] > 1e-32) ? 1.0 / sqrt(SCAL[S_KEPTW]) : 1.0;
-    const int xt = XOFF[P.Q1], yt = YOFF[P.Q1];
-    for (int t = tid; t < xt + yt; t += NT) {
-      bool isX = t < xt;
-      int e = isX ? t : t - xt;
-      int q = blk_find(isX ? XOFF : YOFF, e);
-      int k = KEPT[q], R = THR[q], C = THC[q], n = NQ[q];
-      int loc = e - (isX ? XOFF[q] : YOFF[q]);
-      lzp Tq = TH + THO[q];
-      lzp Wq = Wc + GOFF[q];
-      if (isX) {
-        int row = loc / k, j = loc - row * k;
-        int w = KIDX[EOFF[q] + j];
-        double lam = LAM[EOFF[q] + w];
-        double sig = sqrt(lam);
+    const double kwv = SCAL[S_KEPTW];
+    const double inv = (normalize && kwv > 1e-32) ? 1.0 / sqrt(kwv) : 1.0;
+    const int xt = XOFF[Q1], yt = YOFF[Q1];
+    for (int base = 0; base < xt; base += NT) {
+      const int e = base + tid;
+      const int q = blk(XOFF, e);
+      if (e < xt) {
+        const int k = KEPT[q], C = THC[q], n = NQ[q];
+        int j;
+        const int row = udiv(e - XOFF[q], k, j);
+        const int w = KIDX[EOFF[q] + j];
+        const double sig = sqrt(LAM[EOFF[q] + w]);
+        lzp Tq = TH + THO[q];
+        lzp Wq = Wc + GOFF[q];
         zc out;
         if (SIDE[q] == 0) {
-          out = Wq[row * n + w];                       // u exact
+          out = Wq[row * n + w];  // u exact
           if (dir == kFromright) out = cscale(out, sig * inv);
         } else {
-          zc acc = c2(0, 0);                      // Θ w
+          zc acc = c2(0, 0);  // Θ w
           for (int c = 0; c < C; ++c) cacc(acc, Tq[row * C + c], Wq[c * n + w]);
           if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
-        X[XOFF[q] + loc] = out;
-      } else {
-        int j = loc / C, col = loc - j * C;
-        int w = KIDX[EOFF[q] + j];
-        double lam = LAM[EOFF[q] + w];
-        double sig = sqrt(lam);
+        X[e] = out;
+      }
+    }
+    for (int base = 0; base < yt; base += NT) {
+      const int e = base + tid;
+      const int q = blk(YOFF, e);
+      if (e < yt) {
+        const int R = THR[q], C = THC[q], n = NQ[q];
+        int col;
+        const int j = udiv(e - YOFF[q], C, col);
+        const int w = KIDX[EOFF[q] + j];
+        const double sig = sqrt(LAM[EOFF[q] + w]);
+        lzp Tq = TH + THO[q];
+        lzp Wq = Wc + GOFF[q];
         zc out;
         if (SIDE[q] == 1) {
-          out = cconj(Wq[col * n + w]);                // v^H exact
+          out = cconj(Wq[col * n + w]);  // v^H exact
           if (dir == kFromleft) out = cscale(out, sig * inv);
         } else {
-          zc acc = c2(0, 0);                      // w^H Θ
+          zc acc = c2(0, 0);  // w^H Θ
           for (int r = 0; r < R; ++r) cjacc(acc, Wq[r * n + w], Tq[r * C + col]);
           if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
-        Y[YOFF[q] + loc] = out;
+        Y[e] = out;
       }
     }
     sync();
@@ -739,32 +951,36 @@ struct Chain {
   // write X (rows (n1,a)) into site i1 and Y (cols (n2,c)) into site i1+1
   __device__ OCG_INLINE void scatter_two_site(int i1) {
     pf(6);
-    const int r = i1 + 1, p = P.p;
-    if (tid == 0) {
-      for (int q = 0; q < P.Q1; ++q) DIMS[i1 * P.Q1 + q] = KEPT[q];
-    }
+    const int r = i1 + 1;
+    if (w0 && lane < P.Q1) DIMS[i1 * P.Q1 + lane] = KEPT[lane];
     sync();
-    if (tid == 0) site_offsets_serial(i1, BOFF + (i1 - 1) * P.Q1 * p);
-    if (tid == NT - 1 || NT == 1) site_offsets_serial(r, BOFF + (r - 1) * P.Q1 * p);
+    if (NW == 1) {
+      site_offsets(i1);
+      site_offsets(r);
+    } else if (tid < 64) site_offsets(i1);
+    else if (tid < 128) site_offsets(r);
     sync();
     const int xt = XOFF[P.Q1], yt = YOFF[P.Q1];
-    for (int t = tid; t < xt + yt; t += NT) {
-      bool isX = t < xt;
-      int e = isX ? t : t - xt;
-      int q = blk_find(isX ? XOFF : YOFF, e);
-      int k = KEPT[q];
-      int loc = e - (isX ? XOFF[q] : YOFF[q]);
-      if (isX) {
-        int row = loc / k, j = loc - row * k;
-        int n1 = seg_find(THRO + q * p, row);
-        int ia = row - THRO[q * p + n1];
-        site(i1)[bo(i1, q - n1, n1) + ia * k + j] = X[e];
-      } else {
-        int C = THC[q];
-        int j = loc / C, col = loc - j * C;
-        int n2 = seg_find(THCO + q * p, col);
-        int ic = col - THCO[q * p + n2];
-        site(r)[bo(r, q, n2) + j * d(r, q + n2) + ic] = Y[e];
+    for (int base = 0; base < xt; base += NT) {
+      const int e = base + tid;
+      const int q = blk(XOFF, e);
+      if (e < xt) {
+        const int k = KEPT[q];
+        int j, o;
+        const int row = udiv(e - XOFF[q], k, j);
+        const int n1 = seg_in(TRO, q, row, o);
+        site(i1)[bo(i1, q - n1, n1) + (row - o) * k + j] = X[e];
+      }
+    }
+    for (int base = 0; base < yt; base += NT) {
+      const int e = base + tid;
+      const int q = blk(YOFF, e);
+      if (e < yt) {
+        const int C = THC[q];
+        int col, o;
+        const int j = udiv(e - YOFF[q], C, col);
+        const int n2 = seg_in(TCO, q, col, o);
+        site(r)[bo(r, q, n2) + j * d(r, q + n2) + (col - o)] = Y[e];
       }
     }
     sync();
@@ -775,168 +991,139 @@ struct Chain {
   //   right (Fromright grouping): rows a in bond k-1 sector q, cols (n, c in bond k sector q+n)
   __device__ OCG_INLINE void site_to_theta(int k, bool left) {
     pf(7);
-    const int p = P.p;
-    if (tid == 0) {
-      int off = 0;
-      for (int q = 0; q < P.Q1; ++q) {
-        int R = 0, C = 0;
+    int tot;
+    if (left)
+      tot = theta_tables([&](int q, int n) { return d(k - 1, q - n); },
+                         [&](int q, int n) { return n == 0 ? d(k, q) : 0; });
+    else
+      tot = theta_tables([&](int q, int n) { return n == 0 ? d(k - 1, q) : 0; },
+                         [&](int q, int n) { return d(k, q + n); });
+        for (int base = 0; base < tot; base += NT) {
+      const int e = base + tid;
+      const int q = blk(THO, e);
+      if (e < tot) {
+        const int C = THC[q];
+        int col, o;
+        const int row = udiv(e - THO[q], C, col);
+        zc v;
         if (left) {
-          for (int n = 0; n < p; ++n) { int dl = d(k - 1, q - n); THRO[q * p + n] = dl > 0 ? R : -1; R += dl; }
-          C = d(k, q);
-          for (int n = 0; n < p; ++n) THCO[q * p + n] = -1;
-          THCO[q * p] = C > 0 ? 0 : -1;
+          const int n = seg_in(TRO, q, row, o);
+          v = site(k)[bo(k, q - n, n) + (row - o) * C + col];
         } else {
-          R = d(k - 1, q);
-          for (int n = 0; n < p; ++n) THRO[q * p + n] = -1;
-          THRO[q * p] = R > 0 ? 0 : -1;
-          for (int n = 0; n < p; ++n) {
-            int dr = (q + n <= P.Q) ? d(k, q + n) : 0;
-            THCO[q * p + n] = dr > 0 ? C : -1;
-            C += dr;
-          }
+          const int n = seg_in(TCO, q, col, o);
+          v = site(k)[bo(k, q, n) + row * d(k, q + n) + (col - o)];
         }
-        if (R == 0 || C == 0) { R = 0; C = 0; }
-        THR[q] = R; THC[q] = C; THO[q] = off;
-        off += R * C;
+        TH[e] = v;
       }
-      THO[P.Q1] = off;
-      ISCAL[I_THT] = off;
-    }
-    sync();
-    const int tot = ISCAL[I_THT];
-    for (int e = tid; e < tot; e += NT) {
-      int q = blk_find(THO, e);
-      int loc = e - THO[q], C = THC[q];
-      int row = loc / C, col = loc - row * C;
-      zc v;
-      if (left) {
-        int n = seg_find(THRO + q * p, row);
-        int ia = row - THRO[q * p + n];
-        v = site(k)[bo(k, q - n, n) + ia * C + col];
-      } else {
-        int n = seg_find(THCO + q * p, col);
-        int ic = col - THCO[q * p + n];
-        v = site(k)[bo(k, q, n) + row * d(k, q + n) + ic];
-      }
-      TH[e] = v;
     }
     sync();
   }
 
   // move the orthogonality centre k -> k+1 (ITensor position, one bond)
   __device__ OCG_INLINE void gauge_right(int k, double cutoff, int maxm) {
-    const int p = P.p;
     site_to_theta(k, true);
     decompose(kFromleft, cutoff, maxm, false, MD + k * P.Q1);
     pf(7);
-    // new offsets of site k+1 with new bond-k dims (into BOFFT)
-    if (tid == 0) {
-      int off = 0;
-      for (int q = 0; q < P.Q1; ++q)
-        for (int n = 0; n < p; ++n) {
-          int rr = KEPT[q], cc = (q + n <= P.Q) ? d(k + 1, q + n) : 0;
-          if (rr > 0 && cc > 0) { BOFFT[q * p + n] = off; off += rr * cc; }
-          else BOFFT[q * p + n] = -1;
-        }
-    }
+    // new layout of site k+1 (rows = new bond k) into BOFFT
+    if (w0)
+      scan_excl(BOFFT, SEG, [&](int s) {
+        int q, n;
+        qn_of(s, q, n);
+        return KEPT[q] * d(k + 1, q + n);
+      }, QST);
     sync();
     // S = Y * A_{k+1}   (per (q, n): k_q x d(k+1, q+n))
-    for (int q = 0; q < P.Q1; ++q)
-      for (int n = 0; n < p; ++n) {
-        int o = BOFFT[q * p + n];
-        if (o < 0) continue;
-        int kq = KEPT[q], cc = d(k + 1, q + n), dold = d(k, q);
-        int oo = bo(k + 1, q, n);
-        lzp Yq = Y + YOFF[q];
-        for (int e = tid; e < kq * cc; e += NT) {
-          int i = e / cc, j = e - i * cc;
+    const int ns = BOFFT[SEG];
+    {
+      for (int base = 0; base < ns; base += NT) {
+        const int e = base + tid;
+        int q, n, o;
+        find_qn(BOFFT, e, q, n, o);
+        if (e < ns) {
+          const int cc = d(k + 1, q + n), dold = d(k, q);
+          int c;
+          const int i = udiv(e - o, cc, c);
+          lzp Yq = Y + YOFF[q] + i * dold;
+          lzp Ab = site(k + 1) + bo(k + 1, q, n) + c;
           zc acc = c2(0, 0);
-          if (oo >= 0)
-            for (int b = 0; b < dold; ++b) cacc(acc, Yq[i * dold + b], site(k + 1)[oo + b * cc + j]);
-          S[o + e] = acc;
+          for (int b = 0; b < dold; ++b) cacc(acc, Yq[b], Ab[b * cc]);
+          S[e] = acc;
         }
       }
-    sync();
-    if (tid == 0) {
-      for (int q = 0; q < P.Q1; ++q) DIMS[k * P.Q1 + q] = KEPT[q];
-      site_offsets_serial(k, BOFF + (k - 1) * P.Q1 * p);
-      site_offsets_serial(k + 1, BOFF + k * P.Q1 * p);
     }
+    sync();
+    if (w0 && lane < P.Q1) DIMS[k * P.Q1 + lane] = KEPT[lane];
+    sync();
+    if (w0) site_offsets(k);
+    for (int i = tid; i <= SEG; i += NT) boff(k + 1)[i] = BOFFT[i];
     sync();
     // A_k <- X ; A_{k+1} <- S
     const int xt = XOFF[P.Q1];
-    for (int e = tid; e < xt; e += NT) {
-      int q = blk_find(XOFF, e);
-      int kq = KEPT[q], loc = e - XOFF[q];
-      int row = loc / kq, j = loc - row * kq;
-      int n = seg_find(THRO + q * p, row);
-      int ia = row - THRO[q * p + n];
-      site(k)[bo(k, q - n, n) + ia * kq + j] = X[e];
-    }
-    int ns = 0;
-    for (int q = 0; q < P.Q1; ++q)
-      for (int n = 0; n < p; ++n) {
-        int o = bo(k + 1, q, n);
-        if (o >= 0) { int e = o + d(k, q) * d(k + 1, q + n); if (e > ns) ns = e; }
+    for (int base = 0; base < xt; base += NT) {
+      const int e = base + tid;
+      const int q = blk(XOFF, e);
+      if (e < xt) {
+        const int kq = KEPT[q];
+        int j, o;
+        const int row = udiv(e - XOFF[q], kq, j);
+        const int n = seg_in(TRO, q, row, o);
+        site(k)[bo(k, q - n, n) + (row - o) * kq + j] = X[e];
       }
+    }
     for (int e = tid; e < ns; e += NT) site(k + 1)[e] = S[e];
     sync();
   }
 
   // move the orthogonality centre k -> k-1
   __device__ OCG_INLINE void gauge_left(int k, double cutoff, int maxm) {
-    const int p = P.p;
     site_to_theta(k, false);
     decompose(kFromright, cutoff, maxm, false, MD + (k - 1) * P.Q1);
     pf(7);
-    if (tid == 0) {
-      int off = 0;
-      for (int ql = 0; ql < P.Q1; ++ql)
-        for (int n = 0; n < p; ++n) {
-          int rr = d(k - 2, ql), cc = (ql + n <= P.Q) ? KEPT[ql + n] : 0;
-          if (rr > 0 && cc > 0) { BOFFT[ql * p + n] = off; off += rr * cc; }
-          else BOFFT[ql * p + n] = -1;
-        }
-    }
+    // new layout of site k-1 (cols = new bond k-1) into BOFFT
+    if (w0)
+      scan_excl(BOFFT, SEG, [&](int s) {
+        int ql, n;
+        qn_of(s, ql, n);
+        return (ql + n <= P.Q) ? d(k - 2, ql) * KEPT[ql + n] : 0;
+      }, QST);
     sync();
     // S = A_{k-1} * X   (per (ql, n): d(k-2, ql) x k_{ql+n})
-    for (int ql = 0; ql < P.Q1; ++ql)
-      for (int n = 0; n < p; ++n) {
-        int o = BOFFT[ql * p + n];
-        if (o < 0) continue;
-        int q = ql + n, kq = KEPT[q], rr = d(k - 2, ql), dold = d(k - 1, q);
-        int oo = bo(k - 1, ql, n);
-        lzp Xq = X + XOFF[q];
-        for (int e = tid; e < rr * kq; e += NT) {
-          int i = e / kq, j = e - i * kq;
+    const int ns = BOFFT[SEG];
+    {
+      for (int base = 0; base < ns; base += NT) {
+        const int e = base + tid;
+        int ql, n, o;
+        find_qn(BOFFT, e, ql, n, o);
+        if (e < ns) {
+          const int q = ql + n, kq = KEPT[q], dold = d(k - 1, q);
+          int j;
+          const int i = udiv(e - o, kq, j);
+          lzp Ab = site(k - 1) + bo(k - 1, ql, n) + i * dold;
+          lzp Xq = X + XOFF[q] + j;
           zc acc = c2(0, 0);
-          if (oo >= 0)
-            for (int b = 0; b < dold; ++b) cacc(acc, site(k - 1)[oo + i * dold + b], Xq[b * kq + j]);
-          S[o + e] = acc;
+          for (int b = 0; b < dold; ++b) cacc(acc, Ab[b], Xq[b * kq]);
+          S[e] = acc;
         }
       }
-    sync();
-    if (tid == 0) {
-      for (int q = 0; q < P.Q1; ++q) DIMS[(k - 1) * P.Q1 + q] = KEPT[q];
-      site_offsets_serial(k, BOFF + (k - 1) * P.Q1 * p);
-      site_offsets_serial(k - 1, BOFF + (k - 2) * P.Q1 * p);
     }
+    sync();
+    if (w0 && lane < P.Q1) DIMS[(k - 1) * P.Q1 + lane] = KEPT[lane];
+    sync();
+    if (w0) site_offsets(k);
+    for (int i = tid; i <= SEG; i += NT) boff(k - 1)[i] = BOFFT[i];
     sync();
     const int yt = YOFF[P.Q1];
-    for (int e = tid; e < yt; e += NT) {
-      int q = blk_find(YOFF, e);
-      int C = THC[q], loc = e - YOFF[q];
-      int j = loc / C, col = loc - j * C;
-      int n = seg_find(THCO + q * p, col);
-      int ic = col - THCO[q * p + n];
-      site(k)[bo(k, q, n) + j * d(k, q + n) + ic] = Y[e];
-    }
-    int ns = 0;
-    for (int q = 0; q < P.Q1; ++q)
-      for (int n = 0; n < p; ++n) {
-        int o = bo(k - 1, q, n);
-        if (o >= 0) { int e = o + d(k - 2, q) * d(k - 1, q + n); if (e > ns) ns = e; }
+    for (int base = 0; base < yt; base += NT) {
+      const int e = base + tid;
+      const int q = blk(YOFF, e);
+      if (e < yt) {
+        const int C = THC[q];
+        int col, o;
+        const int j = udiv(e - YOFF[q], C, col);
+        const int n = seg_in(TCO, q, col, o);
+        site(k)[bo(k, q, n) + j * d(k, q + n) + (col - o)] = Y[e];
       }
+    }
     for (int e = tid; e < ns; e += NT) site(k - 1)[e] = S[e];
     sync();
   }
@@ -993,113 +1180,132 @@ struct Chain {
   // Environments are block-diagonal in q: E_q is dX[b][q] x dY[b][q].
   // E0 carries the identity string, E1 the strings with dH already applied
   // (the bond-dimension-2 MPO of propagatorDeriv, src/BH_tDMRG.cpp:10-14).
-  // Scratch: G/G2/W/W2 (environments), X (transfer temp), int tables
-  // XOFF/YOFF (env offsets), BOFFT (temp offsets), THRO (X block offsets).
+  // Per site: T_q = E_q Y_q (Y_q = right-grouped site block, cols (n, c)),
+  // then En_{q'} = sum_n X_(q'-n,n)^H T_(q'-n)[:, (n, .)].
+  // Scratch: G/G2/W/W2 (environments), X/Y (T0/T1), S (staged X site),
+  // XOFF/YOFF (env offsets), BOFFT (X site offsets), TCO/THC/THO (T tables).
   __device__ OCG_INLINE zc overlap(const int* gd, const zc* gx, int with_dH) {
     pf(8);
     const int p = P.p, Q1 = P.Q1;
     lzp E0 = G;  lzp E1 = G2;
     lzp N0 = W;  lzp N1 = W2;
-    LDS int* eo = XOFF;
-    LDS int* no = YOFF;
-    LDS int* to = BOFFT;
-    LDS int* xo = THRO;
-    if (tid == 0) {
-      eo[0] = 0;
-      for (int q = 1; q <= Q1; ++q) eo[q] = 1;  // prefix table: block q=0 is 1x1
-      E0[0] = c2(1, 0);
-      E1[0] = c2(0, 0);
+    for (int i = tid; i < P.nsq; i += NT) DIMX[i] = gd[i];
+    sync();
+    if (w0) {
+      const int q = lane;
+      const int sz = q < Q1 ? dx(0, q) * d(0, q) : 0;
+      const int inc = wscan(sz);
+      if (q < Q1) XOFF[q] = inc - sz;
+      if (lane == 63) { XOFF[Q1] = inc; E0[0] = c2(1, 0); E1[0] = c2(0, 0); }
     }
     sync();
     for (int k = 1; k <= P.L; ++k) {
-      if (tid == 0) {
-        // X block offsets of site k, temp offsets, next-env offsets
-        int ox = 0, ot = 0, oe = 0;
-        for (int q = 0; q < Q1; ++q)
-          for (int n = 0; n < p; ++n) {
-            int rx = gd[(k - 1) * Q1 + q];
-            int cx = (q + n <= P.Q) ? gd[k * Q1 + q + n] : 0;
-            xo[q * p + n] = (rx > 0 && cx > 0) ? ox : -1;
-            if (rx > 0 && cx > 0) ox += rx * cx;
-            int cy = (q + n <= P.Q) ? d(k, q + n) : 0;
-            bool ok = rx > 0 && cx > 0 && d(k - 1, q) > 0 && bo(k, q, n) >= 0;
-            to[q * p + n] = ok ? ot : -1;
-            if (ok) ot += rx * cy;
-          }
-        for (int q = 0; q < Q1; ++q) {  // prefix table (empty blocks have size 0)
-          no[q] = oe;
-          oe += gd[k * Q1 + q] * d(k, q);
+      if (w0) {
+        scan_excl(BOFFT, SEG, [&](int s) {  // X site k block offsets
+          int q, n;
+          qn_of(s, q, n);
+          return dx(k - 1, q) * dx(k, q + n);
+        });
+        scan_excl(TCO, SEG, [&](int s) {  // T column segments (n, c in bond k sector q+n)
+          int q, n;
+          qn_of(s, q, n);
+          return d(k, q + n);
+        });
+      }
+      sync();
+      if (w0) {
+        const int q = lane;
+        int sz = 0, C = 0, nsz = 0;
+        if (q < Q1) {
+          C = TCO[(q + 1) * p] - TCO[q * p];
+          const int rx = dx(k - 1, q), ry = d(k - 1, q);
+          sz = (rx > 0 && ry > 0) ? rx * C : 0;
+          nsz = dx(k, q) * d(k, q);
         }
-        no[Q1] = oe;
+        const int it = wscan(sz), in = wscan(nsz);
+        if (q < Q1) { THC[q] = C; THO[q] = it - sz; YOFF[q] = in - nsz; }
+        if (lane == 63) { THO[Q1] = it; YOFF[Q1] = in; }
       }
-      sync();
-      const int nenv = with_dH ? 2 : 1;
-      // T_(q,n) = E_q * Y_(q,n)   for E0 (and E1): rows dX[k-1][q], cols dY[k][q+n]
-      for (int ev = 0; ev < nenv; ++ev) {
-        lzp E = ev == 0 ? E0 : E1;
-        lzp T = X + ev * (P.thcap / 2);
-        for (int q = 0; q < Q1; ++q)
-          for (int n = 0; n < p; ++n) {
-            int ot = to[q * p + n];
-            if (ot < 0) continue;
-            int rx = gd[(k - 1) * Q1 + q], ry = d(k - 1, q), cy = d(k, q + n);
-            lzp Eq = E + eo[q];
-            lzp Yb = site(k) + bo(k, q, n);
-            for (int e = tid; e < rx * cy; e += NT) {
-              int i = e / cy, j = e - i * cy;
-              zc acc = c2(0, 0);
-              for (int b = 0; b < ry; ++b) cacc(acc, Eq[i * ry + b], Yb[b * cy + j]);
-              T[ot + e] = acc;
-            }
-          }
-      }
-      sync();
-      // En_q' = sum_n f(n) X_(q'-n, n)^H T_(q'-n, n)
+      // stage X site k in LDS: issue the loads before the T contraction, land them after
+      const int nx = BOFFT[SEG];
       const zc* sx = gx + P.site_base[k];
-      const int ne = no[Q1];
-      for (int t = tid; t < nenv * ne; t += NT) {
-        int ev = t >= ne;
-        int e = t - ev * ne;
-        int qq = blk_find(no, e);
-        int cy = d(k, qq);
-        int loc = e - no[qq];
-        int a = loc / cy, j = loc - a * cy;
-        zc acc = c2(0, 0);
-        for (int n = 0; n < p && n <= qq; ++n) {
-          int q = qq - n;
-          int ot = to[q * p + n];
-          if (ot < 0) continue;
-          int rx = gd[(k - 1) * Q1 + q], cx = gd[k * Q1 + qq];
-          const zc* Xb = sx + xo[q * p + n];
-          if (ev == 0) {
-            lzp Tb = X + ot;
-            zc s = c2(0, 0);
-            for (int i = 0; i < rx; ++i) cjacc(s, Xb[i * cx + a], Tb[i * cy + j]);
-            acc = cadd(acc, s);
-          } else {
-            // E1' = X^H (E1 Y) + f(n) X^H (E0 Y)
-            lzp T0 = X + ot;
-            lzp T1 = X + P.thcap / 2 + ot;
-            zc s0 = c2(0, 0), s1 = c2(0, 0);
-            for (int i = 0; i < rx; ++i) {
-              cjacc(s1, Xb[i * cx + a], T1[i * cy + j]);
-              cjacc(s0, Xb[i * cx + a], T0[i * cy + j]);
+      zc pre[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tid + u * NT < nx) pre[u] = sx[tid + u * NT];
+      sync();
+      // T0 = E0_q Y_q -> X buffer, T1 = E1_q Y_q -> Y buffer
+      const int tT = THO[Q1];
+      {
+                for (int base = 0; base < tT; base += NT) {
+          const int e = base + tid;
+          const int q = blk(THO, e);
+          if (e < tT) {
+            const int C = THC[q], ry = d(k - 1, q);
+            int col, o;
+            const int i = udiv(e - THO[q], C, col);
+            const int n = seg_in(TCO, q, col, o);
+            const int cy = d(k, q + n);
+            lzp yb = site(k) + bo(k, q, n) + (col - o);
+            lzp e0 = E0 + XOFF[q] + i * ry;
+            lzp e1 = E1 + XOFF[q] + i * ry;
+            zc t0 = c2(0, 0), t1 = c2(0, 0);
+            for (int b = 0; b < ry; ++b) {
+              const zc yv = yb[b * cy];
+              cacc(t0, e0[b], yv);
+              if (with_dH) cacc(t1, e1[b], yv);
             }
-            acc = cadd(acc, cadd(s1, cscale(s0, P.dH[n])));
+            X[e] = t0;
+            if (with_dH) Y[e] = t1;
           }
         }
-        (ev == 0 ? N0 : N1)[e] = acc;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (tid + u * NT < nx) S[tid + u * NT] = pre[u];
+      for (int i = tid + 4 * NT; i < nx; i += NT) S[i] = sx[i];
+      sync();
+      // En_q' = sum_n X_(q'-n, n)^H T_(q'-n)[:, (n, .)]   (E1 also gets f(n) X^H T0)
+      const int ne = YOFF[Q1];
+      {
+        for (int base = 0; base < ne; base += NT) {
+          const int e = base + tid;
+          const int qq = blk(YOFF, e);
+          if (e < ne) {
+            const int cy = d(k, qq), cx = dx(k, qq);
+            int j;
+            const int a = udiv(e - YOFF[qq], cy, j);
+            zc acc0 = c2(0, 0), acc1 = c2(0, 0);
+            for (int n = 0; n < p && n <= qq; ++n) {
+              const int q = qq - n;
+              const int rx = dx(k - 1, q);
+              if (rx == 0 || d(k - 1, q) == 0) continue;
+              const int C = THC[q];
+              lzp xb = S + BOFFT[q * p + n] + a;
+              const int tc = THO[q] + TCO[q * p + n] - TCO[q * p] + j;
+              zc s0 = c2(0, 0), s1 = c2(0, 0);
+              for (int i = 0; i < rx; ++i) {
+                const zc xv = xb[i * cx];
+                cjacc(s0, xv, X[tc + i * C]);
+                if (with_dH) cjacc(s1, xv, Y[tc + i * C]);
+              }
+              acc0 = cadd(acc0, s0);
+              if (with_dH) acc1 = cadd(acc1, cadd(s1, cscale(s0, P.dH[n])));
+            }
+            N0[e] = acc0;
+            if (with_dH) N1[e] = acc1;
+          }
+        }
       }
       sync();
       lzp t0 = E0; E0 = N0; N0 = t0;
       lzp t1 = E1; E1 = N1; N1 = t1;
-      if (tid == 0)
-        for (int q = 0; q <= Q1; ++q) eo[q] = no[q];
+      for (int i = tid; i <= Q1; i += NT) XOFF[i] = YOFF[i];
       sync();
     }
     zc res = c2(0, 0);
-    int oq = eo[P.Q];
-    if (eo[P.Q1] > oq) res = with_dH ? E1[oq] : E0[oq];
+    const int oq = XOFF[P.Q];
+    if (XOFF[Q1] > oq) res = with_dH ? zc(E1[oq]) : zc(E0[oq]);
     sync();
     return res;
   }
@@ -1114,121 +1320,105 @@ struct Chain {
   __device__ OCG_INLINE void apply_dH(bool truncate_sweep = true) {
     pf(11);
     const int L = P.L, p = P.p, Q1 = P.Q1;
-    LDS int* coff = COFF;   // carry offsets   (Q1+1)
-    LDS int* cdim = CDIM;   // carry rows   = new dims of bond k-1
-    LDS int* cold = COLD;   // carry cols/2 = old dims of bond k-1
-    if (tid == 0) {
-      for (int q = 0; q < Q1; ++q) { cdim[q] = d(0, q); cold[q] = d(0, q); coff[q] = 0; }
-      coff[Q1] = 2;
-      CR[0] = c2(1, 0);  // left boundary of the MPO: s = 0
-      CR[1] = c2(0, 0);
+    if (w0) {
+      const int q = lane;
+      const int dq = q < Q1 ? d(0, q) : 0, sz = 2 * dq * dq;
+      const int inc = wscan(sz);
+      if (q < Q1) { CDIM[q] = dq; COLD[q] = dq; COFF[q] = inc - sz; }
+      if (lane == 63) { COFF[Q1] = inc; CR[0] = c2(1, 0); CR[1] = c2(0, 0); }  // MPO left boundary s = 0
     }
     sync();
     for (int k = 1; k <= L; ++k) {
       const bool last = (k == L);
-      // ---- M_k: rows (n, a' in new bond k-1, sector q-n), cols (t, c in old bond k, sector q)
-      if (tid == 0) {
-        int off = 0;
-        for (int q = 0; q < Q1; ++q) {
-          int R = 0;
-          for (int n = 0; n < p; ++n) {
-            int dl = (q - n >= 0) ? cdim[q - n] : 0;
-            THRO[q * p + n] = dl > 0 ? R : -1;
-            R += dl;
+      // M_k: rows (n, a' in new bond k-1, sector q-n), cols (t, c in old bond k, sector q)
+      const int tot = theta_tables([&](int q, int n) { return (q - n >= 0) ? CDIM[q - n] : 0; },
+                                   [&](int q, int n) { return n == 0 ? (last ? d(k, q) : 2 * d(k, q)) : 0; });
+      {
+                for (int base = 0; base < tot; base += NT) {
+          const int e = base + tid;
+          const int q = blk(THO, e);
+          if (e < tot) {
+            const int C = THC[q];
+            int col, o;
+            const int row = udiv(e - THO[q], C, col);
+            const int n = seg_in(TRO, q, row, o);
+            const int ap = row - o, ql = q - n;
+            const int dc = d(k, q);
+            const int t = last ? 1 : (col >= dc ? 1 : 0);
+            const int c = last ? col : col - t * dc;
+            const int dl = COLD[ql];                          // old rows of A_k blocks
+            lzp Ab = site(k) + bo(k, ql, n) + c;              // dl x dc (old layout)
+            lzp Cq = CR + COFF[ql] + ap * 2 * dl;
+            zc v0 = c2(0, 0), v1 = c2(0, 0);
+            for (int a = 0; a < dl; ++a) {
+              const zc av = Ab[a * dc];
+              cacc(v0, Cq[a], av);
+              cacc(v1, Cq[dl + a], av);
+            }
+            TH[e] = (t == 0) ? v0 : c2(P.dH[n] * v0.x + v1.x, P.dH[n] * v0.y + v1.y);
           }
-          int dc = d(k, q);
-          int C = last ? dc : 2 * dc;
-          for (int n = 0; n < p; ++n) THCO[q * p + n] = -1;
-          THCO[q * p] = C > 0 ? 0 : -1;
-          if (R == 0 || C == 0) { R = 0; C = 0; }
-          THR[q] = R; THC[q] = C; THO[q] = off;
-          off += R * C;
         }
-        THO[Q1] = off;
-        ISCAL[I_THT] = off;
-      }
-      sync();
-      const int tot = ISCAL[I_THT];
-      for (int e = tid; e < tot; e += NT) {
-        int q = blk_find(THO, e);
-        int loc = e - THO[q], C = THC[q];
-        int row = loc / C, col = loc - row * C;
-        int n = seg_find(THRO + q * p, row);
-        int ap = row - THRO[q * p + n];
-        int ql = q - n;
-        int dc = d(k, q);
-        int t = last ? 1 : (col >= dc ? 1 : 0);
-        int c = last ? col : col - t * dc;
-        int dl = cold[ql];                          // old rows of A_k blocks
-        lzp Ab = site(k) + bo(k, ql, n);  // dl x dc (old layout)
-        lzp Cq = CR + coff[ql];
-        int w = 2 * cold[ql];
-        zc v0 = c2(0, 0), v1 = c2(0, 0);
-        for (int a = 0; a < dl; ++a) {
-          zc av = Ab[a * dc + c];
-          cacc(v0, Cq[ap * w + a], av);
-          cacc(v1, Cq[ap * w + cold[ql] + a], av);
-        }
-        TH[e] = (t == 0) ? v0 : c2(P.dH[n] * v0.x + v1.x, P.dH[n] * v0.y + v1.y);
       }
       sync();
       if (last) {
-        if (tid == 0) {
-          for (int q = 0; q < Q1; ++q) DIMS[(L - 1) * Q1 + q] = cdim[q];
-          site_offsets_serial(L, BOFF + (L - 1) * Q1 * p);
-        }
+        if (w0 && lane < Q1) DIMS[(L - 1) * Q1 + lane] = CDIM[lane];
         sync();
-        for (int e = tid; e < tot; e += NT) {
-          int q = blk_find(THO, e);
-          int loc = e - THO[q], C = THC[q];
-          int row = loc / C, col = loc - row * C;
-          int n = seg_find(THRO + q * p, row);
-          int ap = row - THRO[q * p + n];
-          site(L)[bo(L, q - n, n) + ap * C + col] = TH[e];
+        if (w0) site_offsets(L);
+        sync();
+                for (int base = 0; base < tot; base += NT) {
+          const int e = base + tid;
+          const int q = blk(THO, e);
+          if (e < tot) {
+            const int C = THC[q];
+            int col, o;
+            const int row = udiv(e - THO[q], C, col);
+            const int n = seg_in(TRO, q, row, o);
+            site(L)[bo(L, q - n, n) + (row - o) * C + col] = TH[e];
+          }
         }
         sync();
         break;
       }
-      decompose(kFromleft, OCG_GAUGE_CUTOFF, 1 << 30, false, MD + P.nsq + k * P.Q1);
+      decompose(kFromleft, OCG_GAUGE_CUTOFF, 1 << 30, false, MD + P.nsq + k * Q1);
       pf(11);
-      if (tid == 0) {
-        // new layout of site k: rows = new bond k-1 (cdim), cols = KEPT
-        int o2 = 0;
-        for (int q = 0; q < Q1; ++q)
-          for (int n = 0; n < p; ++n) {
-            int r = cdim[q], c = (q + n <= P.Q) ? KEPT[q + n] : 0;
-            if (r > 0 && c > 0) { BOFFT[q * p + n] = o2; o2 += r * c; }
-            else BOFFT[q * p + n] = -1;
-          }
-        ISCAL[12] = o2;
-      }
+      // new layout of site k: rows = new bond k-1 (CDIM), cols = KEPT
+      if (w0)
+        scan_excl(BOFFT, SEG, [&](int s) {
+          int q, n;
+          qn_of(s, q, n);
+          return (q + n <= P.Q) ? CDIM[q] * KEPT[q + n] : 0;
+        });
       sync();
       // S <- X in the new layout of site k; CR <- Y (next carry)
       const int xt = XOFF[Q1], yt = YOFF[Q1];
-      for (int e = tid; e < xt; e += NT) {
-        int q = blk_find(XOFF, e);
-        int kq = KEPT[q], loc = e - XOFF[q];
-        int row = loc / kq, j = loc - row * kq;
-        int n = seg_find(THRO + q * p, row);
-        int ap = row - THRO[q * p + n];
-        S[BOFFT[(q - n) * p + n] + ap * kq + j] = X[e];
+      {
+        for (int base = 0; base < xt; base += NT) {
+          const int e = base + tid;
+          const int q = blk(XOFF, e);
+          if (e < xt) {
+            const int kq = KEPT[q];
+            int j, o;
+            const int row = udiv(e - XOFF[q], kq, j);
+            const int n = seg_in(TRO, q, row, o);
+            S[BOFFT[(q - n) * p + n] + (row - o) * kq + j] = X[e];
+          }
+        }
       }
       for (int e = tid; e < yt; e += NT) CR[e] = Y[e];
       sync();
-      const int ns = ISCAL[12];
+      const int ns = BOFFT[SEG];
       for (int e = tid; e < ns; e += NT) site(k)[e] = S[e];
-      if (tid == 0) {
-        // commit: bond k-1 gets its new dims; bond k keeps the OLD dims
-        // (A_{k+1} is still laid out with them) until site k+1 is rebuilt.
-        if (k > 1)
-          for (int q = 0; q < Q1; ++q) DIMS[(k - 1) * Q1 + q] = cdim[q];
-        for (int i = 0; i < Q1 * p; ++i) BOFF[(k - 1) * Q1 * p + i] = BOFFT[i];
-        for (int q = 0; q < Q1; ++q) {
-          cold[q] = d(k, q);
-          cdim[q] = KEPT[q];
-          coff[q] = YOFF[q];
+      // commit: bond k-1 gets its new dims; bond k keeps the OLD dims
+      // (A_{k+1} is still laid out with them) until site k+1 is rebuilt.
+      for (int i = tid; i <= SEG; i += NT) boff(k)[i] = BOFFT[i];
+      if (w0) {
+        if (lane < Q1) {
+          if (k > 1) DIMS[(k - 1) * Q1 + lane] = CDIM[lane];
+          COLD[lane] = d(k, lane);
+          CDIM[lane] = KEPT[lane];
+          COFF[lane] = YOFF[lane];
         }
-        coff[Q1] = YOFF[Q1];
+        if (lane == 0) COFF[Q1] = YOFF[Q1];
       }
       sync();
     }

@@ -5,6 +5,7 @@
 // loads this code; GPU parity is established by the -m gpu tests.
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -15,9 +16,13 @@
 
 thread_local emu_dim3 threadIdx, blockIdx;
 thread_local std::barrier<>* emu_bar;
+thread_local std::barrier<>* emu_wbar;
 thread_local uint64_t* emu_xbuf;
 
-constexpr int NT = 64;
+#ifndef EMU_NT
+#define EMU_NT 64
+#endif
+constexpr int NT = EMU_NT;
 
 struct Emu {
   OcgParams P;
@@ -43,13 +48,16 @@ static void launch(Emu& e, int grid, const std::function<void(char*)>& body) {
   for (int b = 0; b < grid; ++b) {
     std::vector<ocg::zc> smem((e.lds + 15) / 16 + 1);
     std::barrier<> bar(NT);
-    std::vector<uint64_t> xb(64, 0);
+    std::vector<std::unique_ptr<std::barrier<>>> wb;
+    for (int w = 0; w < NT / 64; ++w) wb.emplace_back(new std::barrier<>(64));
+    std::vector<uint64_t> xb(NT, 0);
     std::vector<std::thread> th;
     for (int t = 0; t < NT; ++t)
       th.emplace_back([&, t, b]() {
         threadIdx.x = t;
         blockIdx.x = b;
         emu_bar = &bar;
+        emu_wbar = wb[t / 64].get();
         emu_xbuf = xb.data();
         body(reinterpret_cast<char*>(smem.data()));
       });

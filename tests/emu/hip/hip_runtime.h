@@ -25,8 +25,9 @@ struct emu_dim3 {
   unsigned x = 0, y = 0, z = 0;
 };
 extern thread_local emu_dim3 threadIdx, blockIdx;
-extern thread_local std::barrier<>* emu_bar;
-extern thread_local uint64_t* emu_xbuf;  // 64-entry exchange buffer of the block
+extern thread_local std::barrier<>* emu_bar;   // workgroup barrier
+extern thread_local std::barrier<>* emu_wbar;  // barrier of this thread's wave
+extern thread_local uint64_t* emu_xbuf;        // exchange buffer of the block (one slot per thread)
 inline void __syncthreads() { emu_bar->arrive_and_wait(); }
 inline int atomicOr(int* p, int v) { return __atomic_fetch_or(p, v, __ATOMIC_SEQ_CST); }
 inline int atomicAdd(int* p, int v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
@@ -39,10 +40,11 @@ inline T emu_xchg(T v, int src) {
   static_assert(sizeof(T) <= 8, "");
   uint64_t b = 0;
   __builtin_memcpy(&b, &v, sizeof(T));
-  emu_xbuf[threadIdx.x & 63] = b;
-  emu_bar->arrive_and_wait();
-  uint64_t r = emu_xbuf[src & 63];
-  emu_bar->arrive_and_wait();
+  const unsigned w = threadIdx.x & ~63u;
+  emu_xbuf[threadIdx.x] = b;
+  emu_wbar->arrive_and_wait();
+  uint64_t r = emu_xbuf[w + (src & 63)];
+  emu_wbar->arrive_and_wait();
   T out;
   __builtin_memcpy(&out, &r, sizeof(T));
   return out;
@@ -64,11 +66,34 @@ inline T __shfl_down(T v, unsigned d, int w = 64) {
 template <class T>
 inline T __shfl_xor(T v, int m, int w = 64) { return emu_xchg(v, (threadIdx.x & 63) ^ m); }
 inline unsigned long long __ballot(int pred) {
-  emu_xbuf[threadIdx.x & 63] = pred ? 1 : 0;
-  emu_bar->arrive_and_wait();
+  const unsigned w = threadIdx.x & ~63u;
+  emu_xbuf[threadIdx.x] = pred ? 1 : 0;
+  emu_wbar->arrive_and_wait();
   unsigned long long m = 0;
-  for (int i = 0; i < 64; ++i) m |= (emu_xbuf[i] ? 1ULL : 0ULL) << i;
-  emu_bar->arrive_and_wait();
+  for (int i = 0; i < 64; ++i) m |= (emu_xbuf[w + i] ? 1ULL : 0ULL) << i;
+  emu_wbar->arrive_and_wait();
   return m;
 }
 inline int __popcll(unsigned long long m) { return __builtin_popcountll(m); }
+inline double rsqrt(double x) { return 1.0 / std::sqrt(x); }
+inline int max(int a, int b) { return a > b ? a : b; }
+inline int min(int a, int b) { return a < b ? a : b; }
+inline long long __double_as_longlong(double v) { long long r; __builtin_memcpy(&r, &v, 8); return r; }
+inline double __longlong_as_double(long long v) { double r; __builtin_memcpy(&r, &v, 8); return r; }
+inline int emu_readlane(int v, int l) { return emu_xchg(v, l); }
+inline float emu_rcpf(float x) { return 1.0f / x; }
+// DPP move: row_shr:n (0x111..0x11f), row_bcast:15 (0x142), row_bcast:31 (0x143);
+// disabled rows and lanes without a source return `old`
+inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int, bool) {
+  const int l = threadIdx.x & 63, row = l >> 4;
+  int s = -1;
+  if (ctrl > 0x110 && ctrl < 0x120) { int n = ctrl - 0x110; if ((l & 15) >= n) s = l - n; }
+  else if (ctrl == 0x142) { if (row >= 1) s = row * 16 - 1; }
+  else if (ctrl == 0x143) { if (row >= 2) s = 31; }
+  int v = emu_xchg(src, s < 0 ? l : s);
+  if (!((row_mask >> row) & 1) || s < 0) return old;
+  return v;
+}
+#define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
+#define __builtin_amdgcn_rcpf(x) emu_rcpf(x)
+#define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))

@@ -2,15 +2,18 @@
 import os, sys, subprocess, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-lib = "/tmp/libocg_prof.so"
+NT = int(os.environ.get("OCG_PROF_NT", "64"))
+lib = f"/tmp/libocg_prof{NT}.so"
 subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                       "-DOCG_PROFILE", "-o", lib, os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip")])
+                       "-DOCG_PROFILE", f"-DOCG_NT={NT}", "-o", lib,
+                       os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip")])
+print(f"NT = {NT}")
 os.environ["OCG_LIB"] = lib
 import numpy as np
 from optimalcontrolmps_amd import ed
 from optimalcontrolmps_amd.native import MPS, Engine
 NAMES = ["build_theta", "apply_gate", "gram", "jacobi", "rank/trunc", "factors", "scatter", "gauge wb", "overlap",
-         "phase/norm", "load/store", "dH zip", "other"]
+         "phase/norm", "load/store", "dH zip", "other", "jacobi A", "jacobi B", "theta tabs", "decomp setup"]
 L, p, Q, J, dt = 5, 5, 5, 1.0, 0.01
 ini = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, 2.5)[0], L, p, Q))
 tgt = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, 50.0)[0], L, p, Q))
@@ -28,9 +31,11 @@ for what in ["trajectory(2 chains x 200 steps)", "div_t+xi_dH", "hessian_rows(19
         H = eng.hessian_rows(u, list(range(1, 200)), F, d)
     t1 = time.perf_counter()
     pr = eng.profile(True)
-    tot = pr[:13].sum()
+    tot = pr[:17].sum()
     print(f"== {what}: wall {1e3*(t1-t0):.1f} ms, total cycles {tot:.3e}")
     for i, n in enumerate(NAMES):
         if pr[i] > 0:
             print(f"   {n:12s} {pr[i]:.3e} ({100*pr[i]/tot:5.1f}%)")
+    if pr[21] > 0:
+        print(f"   jacobi calls {pr[21]:.0f}, sweeps/call {pr[20]/pr[21]:.2f}, rounds/sweep {pr[22]/pr[21]:.2f}")
 print("traj kernel ms:", eng.stats(0)["ms"], " rows ms:", eng.stats(3)["ms"])
