@@ -32,19 +32,6 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFS = 78.6       # MI355X FP64 vector/matrix spec
 
 
-def zigzag_rows(nrows_total, rank, world):
-    """rows 1..N-2, row i costs N-2-i steps: serpentine assignment balances load"""
-    rows = list(range(1, nrows_total + 1))
-    out = []
-    for blk in range(0, len(rows), world):
-        chunk = rows[blk:blk + world]
-        if (blk // world) % 2 == 1:
-            chunk = chunk[::-1]
-        if rank < len(chunk):
-            out.append(chunk[rank])
-    return out
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -68,6 +55,7 @@ def main():
 
     from optimalcontrolmps_amd import ed
     from optimalcontrolmps_amd.native import MPS, Engine
+    from optimalcontrolmps_amd.sharding import zigzag_rows
 
     L, p, Q, J, dt = CFG["L"], CFG["p"], CFG["npart"], CFG["J"], CFG["tstep"]
     Nt = int(round(CFG["T"] / dt)) + 1

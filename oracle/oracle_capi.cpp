@@ -142,6 +142,26 @@ int orc_oc_hessian(void* o, const double* u, int threads, double* out) {
   std::memcpy(out, H.data(), H.size() * sizeof(double));
   return 0;
 }
+// Fidelity-Hessian entries of the given rows only (psi, xi, divT and xiH are
+// recomputed for u; no regularisation): the per-rank shard of a row-sharded
+// getHessian, written into a zeroed N x N `out`.
+int orc_oc_rows(void* o, const double* u, const int* rows, int nrows, double* out) {
+  auto& oc = *static_cast<OrcOC*>(o)->oc;
+  std::vector<double> uu(u, u + oc.N);
+  oc.calcPsi(uu);
+  oc.calcXi(uu);
+  oc.calcDivT();
+  oc.xiH.assign(oc.N, MPS());
+  for (size_t i = 0; i < oc.N; ++i) oc.xiH[i] = oc.st.apply_dH(oc.xi_t[i]);
+  std::vector<double> H(oc.N * oc.N, 0.0);
+  const cplx F = oc.overlapFactor();
+  for (int r = 0; r < nrows; ++r) {
+    if (rows[r] < 1 || size_t(rows[r]) + 1 >= oc.N) return 1;
+    oc.hessianRow(size_t(rows[r]), uu, F, H);
+  }
+  std::memcpy(out, H.data(), H.size() * sizeof(double));
+  return 0;
+}
 // which: 0 = psi_t, 1 = xi_t, 2 = xiH
 int orc_oc_state(void* o, int which, int t, int* fd, double* data, size_t cap, size_t* nelem) {
   auto& oc = *static_cast<OrcOC*>(o)->oc;

@@ -1,0 +1,439 @@
+// TEST DRIVER — restates the reference's C++ test programs
+// (tests/ControlBasisTests.cpp, CostTests.cpp, GradientTests.cpp,
+// HessianTests.cpp, SequencingTest.cpp) against the optimalcontrolmps facade
+// (optimalcontrolmps_amd/include/optimalcontrolmps/OptimalControl.hpp).
+//
+// Built twice by tests/facade_build.py:
+//   -DOCMPS_ORACLE : OptimalControl<OracleTDMRG> (CPU restatement; -m "not gpu")
+//   (default)      : OptimalControl<GpuTDMRG> over liboptimalcontrolmps_amd.so (-m gpu)
+// Usage: facade_driver <scenario> <state-dir>; prints one JSON object with the
+// computed quantities, which tests/test_facade*.py compare against the
+// reference's golden values and tolerances.  States are ED ground states
+// written by the tests from tests/golden/states.npz (<key>.bin).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <functional>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/ControlBasisFactory.hpp"
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/OptimalControl.hpp"
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/SeedGenerator.hpp"
+
+#ifdef OCMPS_ORACLE
+#include "oracle_stepper.hpp"
+using Stepper = ocmps_test::OracleTDMRG;
+#else
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/GpuTDMRG.hpp"
+using Stepper = ocmps::GpuTDMRG;
+#endif
+
+using ocmps::Args;
+using ocmps::BoseHubbard;
+using ocmps::Cplx;
+using ocmps::MPS;
+using ocmps::rowmat;
+using ocmps::stdvec;
+using OC = OptimalControl<Stepper>;
+
+static std::string g_dir;
+
+// ---------------------------------------------------------------- output
+struct Json {
+  std::ostringstream o;
+  bool first = true;
+  void key(const std::string& k) {
+    o << (first ? "{" : ", ") << "\"" << k << "\": ";
+    first = false;
+  }
+  void num(const std::string& k, double v) {
+    key(k);
+    char b[64];
+    std::snprintf(b, sizeof b, "%.17g", v);
+    o << b;
+  }
+  void vec(const std::string& k, const stdvec& v) {
+    key(k);
+    o << "[";
+    for (size_t i = 0; i < v.size(); ++i) {
+      char b[64];
+      std::snprintf(b, sizeof b, "%.17g", v[i]);
+      o << (i ? ", " : "") << b;
+    }
+    o << "]";
+  }
+  void mat(const std::string& k, const rowmat& m) {
+    key(k);
+    o << "[";
+    for (size_t i = 0; i < m.size(); ++i) {
+      o << (i ? ", " : "") << "[";
+      for (size_t j = 0; j < m[i].size(); ++j) {
+        char b[64];
+        std::snprintf(b, sizeof b, "%.17g", m[i][j]);
+        o << (j ? ", " : "") << b;
+      }
+      o << "]";
+    }
+    o << "]";
+  }
+  void flag(const std::string& k, bool v) {
+    key(k);
+    o << (v ? "true" : "false");
+  }
+  std::string str() { return o.str() + (first ? "{}" : "}"); }
+};
+
+// ---------------------------------------------------------------- inputs
+static MPS load_state(const std::string& key) {
+  std::ifstream f(g_dir + "/" + key + ".bin", std::ios::binary);
+  if (!f) throw std::runtime_error("missing state " + key);
+  int h[5];
+  f.read(reinterpret_cast<char*>(h), sizeof h);
+  std::vector<int> dims(h[3]);
+  f.read(reinterpret_cast<char*>(dims.data()), sizeof(int) * h[3]);
+  std::vector<Cplx> data(h[4]);
+  f.read(reinterpret_cast<char*>(data.data()), sizeof(double) * 2 * h[4]);
+  return MPS(h[0], h[1], h[2], dims, data);
+}
+static std::string skey(int L, int p, int N, double J, double U) {
+  char b[96];
+  std::snprintf(b, sizeof b, "L%d_p%d_N%d_J%g_U%g", L, p, N, J, U);
+  return b;
+}
+// reference test helpers: rand()-based iid controls (tests/GradientTests.cpp:87-105)
+static stdvec randseed(double lo, double hi, int n) {
+  stdvec v;
+  for (int i = 0; i < n; ++i) v.push_back(lo + (double)rand() / RAND_MAX * (hi - lo));
+  return v;
+}
+static stdvec numeric_grad(stdvec c, OC& oc) {  // central differences, eps 1e-5 (:107-128)
+  const double eps = 1e-5;
+  stdvec g;
+  for (auto& ui : c) {
+    ui += eps;
+    const double jp = oc.getCost(c);
+    ui -= 2 * eps;
+    const double jm = oc.getCost(c);
+    ui += eps;
+    g.push_back((jp - jm) / (2 * eps));
+  }
+  return g;
+}
+static rowmat numeric_hessian(stdvec c, OC& oc) {  // forward differences, eps 1e-3 (HessianTests.cpp:107-139)
+  const size_t n = c.size();
+  const double eps = 1e-3;
+  rowmat H(n, stdvec(n, 0.0));
+  const double fx = oc.getCost(c);
+  stdvec fe(n);
+  for (size_t i = 0; i < n; ++i) {
+    c[i] += eps;
+    fe[i] = oc.getCost(c);
+    c[i] -= eps;
+  }
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = i; j < n; ++j) {
+      c[i] += eps;
+      c[j] += eps;
+      H[i][j] = H[j][i] = (oc.getCost(c) - fe[i] - fe[j] + fx) / (eps * eps);
+      c[i] -= eps;
+      c[j] -= eps;
+    }
+  return H;
+}
+
+// ---------------------------------------------------------------- scenarios
+// tests/ControlBasisTests.cpp: SimpleMatrixTest (:9-27) and ChoppedSineTest (:30-50)
+static void scen_basis(Json& js) {
+  {
+    stdvec u0(5, 1.0), S(5, 1.0);
+    rowmat f(5, stdvec(4, 2.0));
+    ControlBasis b(u0, S, f);
+    js.vec("simple_u_c0", b.convertControl(stdvec(4, 0.0)));
+    js.vec("simple_u_c1", b.convertControl(stdvec(4, 1.0)));
+    js.vec("simple_u_cached", b.convertControl(stdvec(4, 0.0), false));
+    js.vec("simple_g0", b.convertGradient(stdvec(5, 0.0)));
+    js.vec("simple_g1", b.convertGradient(stdvec(5, 1.0)));
+    js.mat("simple_jac", b.getControlJacobian());
+    js.mat("simple_h1", b.convertHessian(rowmat(5, stdvec(5, 1.0))));
+  }
+  stdvec u0 = {1, 1.1, 1.2, 1.3, 1.4, 1.5, 1.6, 1.7, 1.8, 1.9, 2};
+  ControlBasis b = ControlBasisFactory::buildChoppedSineBasis(u0, 0.1, 1.0, 5);
+  js.vec("cs_u_c0", b.convertControl(stdvec(5, 0.0)));
+  js.vec("cs_u_c1", b.convertControl(stdvec(5, 1.0)));
+  js.vec("cs_u_cached", b.convertControl(stdvec(5, 0.0), false));
+  js.vec("cs_g0", b.convertGradient(stdvec(11, 0.0)));
+  js.vec("cs_g1", b.convertGradient(stdvec(11, 1.0)));
+  js.mat("cs_jac", b.getControlJacobian());
+  js.mat("cs_h0", b.convertHessian(rowmat(11, stdvec(11, 0.0))));
+  js.mat("cs_h1", b.convertHessian(rowmat(11, stdvec(11, 1.0))));
+  rowmat h3(11, stdvec(11, 1.0));
+  double idx = 0.0;
+  for (size_t i = 0; i < 11; ++i)
+    for (size_t j = i; j < 11; ++j) {
+      h3[i][j] = h3[j][i] = idx;
+      idx += 0.01;
+    }
+  js.mat("cs_h3", b.convertHessian(h3));
+  js.vec("linspace", SeedGenerator::linspace(0, 1, 11));
+  stdvec x = SeedGenerator::linspace(0, 100, 11);
+  js.vec("sigmoid", SeedGenerator::sigmoid(x, 8.0, 1.1));
+  js.vec("adiabatic", SeedGenerator::adiabaticSeed(2.0, 50.0, 11));
+}
+
+// tests/CostTests.cpp:14-66 fixture: L=5, Npart=5, locDim=5, J=1, U 2 -> 50, T=0.1, dt=0.01, M=5
+static void scen_cost(Json& js) {
+  BoseHubbard sites(5, 5);
+  MPS ini = load_state(skey(5, 6, 5, 1.0, 2.0)), tgt = load_state(skey(5, 6, 5, 1.0, 50.0));
+  Stepper st(sites, 1.0, 0.01, Args(1e-8));
+  const int N = 11, M = 5;
+  stdvec u0 = SeedGenerator::linspace(2.0, 50.0, N);
+  ControlBasis basis = ControlBasisFactory::buildChoppedSineBasis(u0, 0.01, 0.1, M);
+  OC grape(tgt, ini, st, N, 0), group(tgt, ini, st, basis, 0);
+  for (int reg = 0; reg < 2; ++reg) {
+    const std::string s = reg ? "_reg" : "";
+    grape.setGamma(reg);
+    group.setGamma(reg);
+    js.num("grape_lin_cost" + s, grape.getCost(u0));
+    js.vec("grape_lin_fid" + s, grape.getFidelityForAllT(u0, false));
+    stdvec ones(N, 1.0);
+    js.num("grape_ones_cost" + s, grape.getCost(ones));
+    js.vec("grape_ones_fid" + s, grape.getFidelityForAllT(ones, false));
+    stdvec c0(M, 0.0);
+    js.num("group_c0_cost" + s, group.getCost(c0));
+    js.vec("group_c0_fid" + s, group.getFidelityForAllT(c0, false));
+    stdvec c1 = SeedGenerator::linspace(0, 7, M);
+    js.num("group_lin_cost" + s, group.getCost(c1));
+    js.vec("group_lin_fid" + s, group.getFidelityForAllT(c1, false));
+  }
+  js.vec("time_axis", grape.getTimeAxis());
+  js.mat("grape_jac", grape.getControlJacobian());
+}
+
+// tests/GradientTests.cpp:17-50 fixture: L=5, locDim=5, U 2 -> 12, T=0.15, dt=0.01, M=10
+static void scen_gradient(Json& js) {
+  srand(20261015);
+  BoseHubbard sites(5, 5);
+  MPS ini = load_state(skey(5, 6, 5, 1.0, 2.0)), tgt = load_state(skey(5, 6, 5, 1.0, 12.0));
+  Stepper st(sites, 1.0, 0.01, Args(1e-8));
+  const int N = 16, M = 10;
+  stdvec u0 = SeedGenerator::linspace(2.0, 12.0, N);
+  ControlBasis basis = ControlBasisFactory::buildChoppedSineBasis(u0, 0.01, 0.15, M);
+  for (int bfgs = 0; bfgs < 2; ++bfgs) {
+    const std::string s = bfgs ? "_bfgs" : "";
+    {
+      OC oc(tgt, ini, st, N, 0);
+      oc.setBFGS(bfgs);
+      stdvec c = randseed(2, 10, N);
+      js.vec("grape_num" + s, numeric_grad(c, oc));
+      js.vec("grape_ana" + s, oc.getAnalyticGradient(c));
+      oc.setGamma(1);
+      js.vec("grape_ana_reg" + s, oc.getAnalyticGradient(c, false));
+      js.vec("grape_num_reg" + s, numeric_grad(c, oc));
+    }
+    {
+      OC oc(tgt, ini, st, basis, 0);
+      oc.setBFGS(bfgs);
+      stdvec c = randseed(-4, 4, M);
+      js.vec("group_num" + s, numeric_grad(c, oc));
+      js.vec("group_ana" + s, oc.getAnalyticGradient(c));
+      oc.setGamma(1);
+      js.vec("group_ana_reg" + s, oc.getAnalyticGradient(c, false));
+      js.vec("group_num_reg" + s, numeric_grad(c, oc));
+    }
+  }
+  // testSequencialVsParallel (:250-285)
+  OC oc(tgt, ini, st, N, 0);
+  stdvec c = randseed(2, 10, N);
+  stdvec seq = oc.getAnalyticGradient(c);
+  oc.setThreadCount(2);
+  js.vec("grad_seq", seq);
+  js.vec("grad_par", oc.getAnalyticGradient(c));
+  oc.setBFGS(true);
+  js.vec("grad_par_bfgs", oc.getAnalyticGradient(c));
+  oc.setThreadCount(1);
+  js.vec("grad_seq_bfgs", oc.getAnalyticGradient(c));
+}
+
+// tests/HessianTests.cpp:16-50 fixture: L=5, locDim=5, U 2 -> 12, T=0.1, dt=0.01, M=8
+static void scen_hessian(Json& js) {
+  srand(7);
+  BoseHubbard sites(5, 5);
+  MPS ini = load_state(skey(5, 6, 5, 1.0, 2.0)), tgt = load_state(skey(5, 6, 5, 1.0, 12.0));
+  Stepper st(sites, 1.0, 0.01, Args(1e-8));
+  const int N = 11, M = 8;
+  stdvec u0 = SeedGenerator::linspace(2.0, 12.0, N);
+  ControlBasis basis = ControlBasisFactory::buildChoppedSineBasis(u0, 0.01, 0.1, M);
+  {
+    OC oc(tgt, ini, st, N, 0);
+    stdvec c = randseed(2, 10, N);
+    js.mat("grape_ana", oc.getHessian(c));
+    js.mat("grape_num", numeric_hessian(c, oc));
+    oc.setGamma(1);
+    js.mat("grape_ana_reg", oc.getHessian(c, false));
+    js.mat("grape_num_reg", numeric_hessian(c, oc));
+  }
+  {
+    OC oc(tgt, ini, st, basis, 0);
+    stdvec c = randseed(-2, 2, M);
+    js.mat("group_ana", oc.getHessian(c));
+    js.mat("group_num", numeric_hessian(c, oc));
+    oc.setGamma(1);
+    js.mat("group_ana_reg", oc.getHessian(c, false));
+    js.mat("group_num_reg", numeric_hessian(c, oc));
+  }
+  // testSequencialVsParallel (:254-269)
+  OC oc(tgt, ini, st, N, 0);
+  stdvec c = randseed(2, 10, N);
+  js.mat("hess_seq", oc.getHessian(c));
+  oc.setThreadCount(2);
+  js.mat("hess_par", oc.getHessian(c));
+}
+
+// tests/SequencingTest.cpp:14-40 fixture: L=3, Npart=3, locDim=3, J=2, U 2 -> 12, T=0.5, cutoff 1e-7
+static void scen_sequencing(Json& js) {
+  srand(11);
+  BoseHubbard sites(3, 3);
+  MPS ini = load_state(skey(3, 4, 3, 2.0, 2.0)), tgt = load_state(skey(3, 4, 3, 2.0, 12.0));
+  Stepper st(sites, 2.0, 0.01, Args(1e-7));
+  const int N = 51;
+  const stdvec c0 = randseed(5, 15, N);
+  const stdvec cA = randseed(2, 20, N), cB = randseed(1, 4, N);
+  auto same = [](double a, double b) { return std::fabs(a - b) < 1e-10; };
+  auto sameg = [](const stdvec& a, const stdvec& b) {
+    for (size_t i = 0; i < a.size(); ++i)
+      if (std::fabs(a[i] - b[i]) > 1e-10) return false;
+    return true;
+  };
+  auto sameh = [](const rowmat& a, const rowmat& b) {
+    for (size_t i = 0; i < a.size(); ++i)
+      for (size_t j = 0; j < a[i].size(); ++j)
+        if (std::fabs(a[i][j] - b[i][j]) > 1e-10) return false;
+    return true;
+  };
+  struct Init {
+    double cost;
+    stdvec grad;
+    rowmat hess;
+  };
+  auto fresh = [&](std::unique_ptr<OC>& oc) {
+    oc.reset(new OC(tgt, ini, st, N, 0));
+    Init r;
+    r.cost = oc->getCost(c0, true);
+    r.grad = oc->getAnalyticGradient(c0, true);
+    r.hess = oc->getHessian(c0, true);
+    return r;
+  };
+  std::unique_ptr<OC> oc;
+  // six orderings of cost / gradient / Hessian on the same control (:81-203)
+  const char* orders[] = {"CGH", "GCH", "CHG", "GHC", "HGC", "HCG"};
+  for (const char* ord : orders) {
+    Init r = fresh(oc);
+    double c = 0;
+    stdvec g;
+    rowmat h;
+    for (int k = 0; k < 3; ++k) {
+      const bool nc = (k == 0);
+      if (ord[k] == 'C') c = oc->getCost(c0, nc);
+      if (ord[k] == 'G') g = oc->getAnalyticGradient(c0, nc);
+      if (ord[k] == 'H') h = oc->getHessian(c0, nc);
+    }
+    js.flag(std::string("same_") + ord, same(r.cost, c) && sameg(r.grad, g) && sameh(r.hess, h));
+    if (std::string(ord) == "CGH" || std::string(ord) == "GCH") {
+      oc->setBFGS(true);
+      if (ord[0] == 'C') {
+        c = oc->getCost(c0, true);
+        g = oc->getAnalyticGradient(c0, false);
+      } else {
+        g = oc->getAnalyticGradient(c0, true);
+        c = oc->getCost(c0, false);
+      }
+      js.flag(std::string("same_bfgs_") + ord, same(r.cost, c) && sameg(r.grad, g));
+    }
+  }
+  {  // testNewControl_Cost (:205-216)
+    Init r = fresh(oc);
+    const double nc = oc->getCost(cA, true);
+    oc->setBFGS(true);
+    const double nc2 = oc->getCost(cA, true);
+    js.flag("new_cost", !same(r.cost, nc) && !same(r.cost, nc2) && same(nc, nc2));
+  }
+  {  // testNewControl_Grad (:218-229)
+    Init r = fresh(oc);
+    const stdvec g1 = oc->getAnalyticGradient(cA, true);
+    oc->setBFGS(true);
+    const stdvec g2 = oc->getAnalyticGradient(cA, true);
+    js.flag("new_grad", !sameg(r.grad, g1) && !sameg(r.grad, g2) && sameg(g1, g2));
+  }
+  {  // testNewControl_Hess (:231-236)
+    Init r = fresh(oc);
+    js.flag("new_hess", !sameh(r.hess, oc->getHessian(cA, true)));
+  }
+  {  // testNewControl_CostCost (:238-245)
+    Init r = fresh(oc);
+    const double f = oc->getCost(cA, false), t = oc->getCost(cA, true);
+    js.flag("new_cost_cost", same(r.cost, f) && !same(t, f));
+  }
+  {  // testNewControl_GradGrad (:247-254)
+    Init r = fresh(oc);
+    const stdvec f = oc->getAnalyticGradient(cA, false), t = oc->getAnalyticGradient(cA, true);
+    js.flag("new_grad_grad", sameg(r.grad, f) && !sameg(t, f));
+  }
+  {  // testNewControl_HessHess (:256-263)
+    Init r = fresh(oc);
+    const rowmat f = oc->getHessian(cB, false), t = oc->getHessian(cB, true);
+    js.flag("new_hess_hess", !sameh(r.hess, f) && !sameh(t, f));
+  }
+}
+
+// one getHessian on caller-chosen controls (GPU parity against the oracle driver)
+static void scen_golden(Json& js) {
+  BoseHubbard sites(5, 4);
+  MPS ini = load_state(skey(5, 5, 5, 1.0, 2.5)), tgt = load_state(skey(5, 5, 5, 1.0, 50.0));
+  Stepper st(sites, 1.0, 0.01, Args(1e-8, 80));
+  const int N = 21;
+  stdvec u;
+  for (int i = 0; i < N; ++i) u.push_back(2.0 + 8.0 * std::fabs(std::sin(0.37 * i + 0.1)));
+  OC oc(tgt, ini, st, N, 1e-6);
+  js.num("cost", oc.getCost(u));
+  js.vec("grad", oc.getAnalyticGradient(u, false));
+  js.mat("hess", oc.getHessian(u, false));
+  js.vec("fid", oc.getFidelityForAllT(u, false));
+  std::vector<MPS> traj = oc.getPsit();
+  stdvec bd;
+  for (int b = 0; b <= 5; ++b) bd.push_back(traj.back().bondDim(b));
+  js.vec("psiT_bond_dims", bd);
+  // a single stepper step through the TimeStepper concept (BH_tDMRG::step)
+  MPS s = ini;
+  st.step(s, 2.0, 3.0, true);
+  st.step(s, 3.0, 2.0, false);
+  stdvec bd2;
+  for (int b = 0; b <= 5; ++b) bd2.push_back(s.bondDim(b));
+  js.vec("step_bond_dims", bd2);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    std::fprintf(stderr, "usage: %s <basis|cost|gradient|hessian|sequencing|golden> <state-dir>\n", argv[0]);
+    return 2;
+  }
+  g_dir = argv[2];
+  const std::string sc = argv[1];
+  Json js;
+  try {
+    if (sc == "basis") scen_basis(js);
+    else if (sc == "cost") scen_cost(js);
+    else if (sc == "gradient") scen_gradient(js);
+    else if (sc == "hessian") scen_hessian(js);
+    else if (sc == "sequencing") scen_sequencing(js);
+    else if (sc == "golden") scen_golden(js);
+    else throw std::runtime_error("unknown scenario " + sc);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    return 1;
+  }
+  std::printf("%s\n", js.str().c_str());
+  return 0;
+}

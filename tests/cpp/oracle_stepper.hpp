@@ -1,0 +1,102 @@
+// TEST INFRASTRUCTURE ONLY — the CPU oracle (oracle/tdmrg_oracle.hpp) behind
+// the facade's TimeStepper concept, so the host logic of OptimalControl
+// (caching, regularisation, GRAPE/GROUP, BFGS, threadCount) is tested on
+// CPU by the same driver that the GPU build runs.  Never part of the product.
+#pragma once
+
+#include <memory>
+#include <thread>
+
+#include "../../oracle/tdmrg_oracle.hpp"
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/MPS.hpp"
+
+namespace ocmps_test {
+
+using ocmps::Cplx;
+using ocmps::MPS;
+using ocmps::rowmat;
+using ocmps::stdvec;
+
+inline oracle::MPS to_oracle(const MPS& m) {
+  return oracle::MPS::from_flat(m.L, m.p, m.Q, m.dims.data(), m.raw());
+}
+inline MPS from_oracle(const oracle::MPS& m) {
+  std::vector<int> d;
+  std::vector<double> x;
+  m.to_flat(d, x);
+  std::vector<Cplx> z(x.size() / 2);
+  for (size_t i = 0; i < z.size(); ++i) z[i] = Cplx(x[2 * i], x[2 * i + 1]);
+  return MPS(m.L, m.p, m.Q, d, z);
+}
+
+class OracleTDMRG {
+ public:
+  class Engine;
+  OracleTDMRG(const ocmps::BoseHubbard& sites, double J_, double tstep_, const ocmps::Args& a = ocmps::Args())
+      : L(sites.L), p(sites.localDim()), J(J_), tstep(tstep_), args(a) {}
+  double getTstep() const { return tstep; }
+  ocmps::Args getArgs() const { return args; }
+  oracle::Stepper stepper(int Q) const { return oracle::Stepper(L, p, Q, J, tstep, args.cutoff, args.maxm > 0 ? args.maxm : 5000); }
+  void step(MPS& psi, double from, double to, bool forward = true) const {
+    oracle::MPS m = to_oracle(psi);
+    stepper(psi.Q).step(m, from, to, forward);
+    psi = from_oracle(m);
+  }
+  std::unique_ptr<Engine> makeEngine(const MPS& target, const MPS& init, size_t N) const;
+
+ private:
+  int L, p;
+  double J, tstep;
+  ocmps::Args args;
+};
+
+class OracleTDMRG::Engine {
+ public:
+  Engine(const oracle::Stepper& st, const MPS& tgt, const MPS& ini, size_t N_)
+      : oc(st, to_oracle(tgt), to_oracle(ini), N_, 0.0), N(N_) {}
+  void setShards(size_t n) { threads = int(n); }
+  void propagate(const stdvec& u, int which) {
+    if (which == 3 && threads > 1) {  // calcPsiXiDivT's two threads (:421-438)
+      std::thread a([&]() { oc.calcPsi(u); }), b([&]() { oc.calcXi(u); });
+      a.join();
+      b.join();
+      return;
+    }
+    if (which & 1) oc.calcPsi(u);
+    if (which & 2) oc.calcXi(u);
+  }
+  std::vector<Cplx> divT() {
+    oc.calcDivT();
+    return oc.divT;
+  }
+  Cplx overlapFactor() { return oc.overlapFactor(); }
+  stdvec fidelities() { return oc.fidelities(); }
+  void precomputeXiH() {
+    oc.xiH.assign(N, oracle::MPS());
+    for (size_t i = 0; i < N; ++i) oc.xiH[i] = oc.st.apply_dH(oc.xi_t[i]);
+  }
+  void hessianRows(const stdvec& u, Cplx F, const std::vector<Cplx>& dT, rowmat& H) {
+    oc.divT = dT;
+    std::vector<double> h(N * N, 0.0);
+    oc.rows(u, F, h, threads);
+    for (size_t i = 0; i < N; ++i)
+      for (size_t j = 0; j < N; ++j) H[i][j] += h[i * N + j];
+  }
+  std::vector<MPS> psiTrajectory() {
+    std::vector<MPS> out;
+    for (auto& m : oc.psi_t) out.push_back(from_oracle(m));
+    return out;
+  }
+
+ private:
+  oracle::OC oc;
+  size_t N;
+  int threads = 1;
+};
+
+inline std::unique_ptr<OracleTDMRG::Engine> OracleTDMRG::makeEngine(const MPS& target, const MPS& init,
+                                                                    size_t N) const {
+  return std::unique_ptr<Engine>(new Engine(stepper(target.Q), target, init, N));
+}
+
+}  // namespace ocmps_test

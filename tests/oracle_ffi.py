@@ -54,6 +54,7 @@ def lib():
         L.orc_oc_gradient.argtypes = [C.c_void_p, dp, C.c_int, dp]
         L.orc_oc_divT.argtypes = [C.c_void_p, dp, dp]
         L.orc_oc_hessian.argtypes = [C.c_void_p, dp, C.c_int, dp]
+        L.orc_oc_rows.argtypes = [C.c_void_p, dp, ip, C.c_int, dp]
         L.orc_oc_state.argtypes = [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.orc_oc_time_hessian.restype = C.c_double
         L.orc_oc_time_hessian.argtypes = [C.c_void_p, dp, C.c_int, dp]
@@ -199,6 +200,15 @@ class OC:
         uu, pu = _d(u)
         out = np.zeros(self.N * self.N)
         lib().orc_oc_hessian(self.h, pu, threads, out.ctypes.data_as(dp))
+        return out.reshape(self.N, self.N)
+
+    def rows(self, u, rows):
+        """fidelity-Hessian entries of the given rows only (one rank's shard)"""
+        uu, pu = _d(u)
+        rr = np.ascontiguousarray(rows, dtype=np.int32)
+        out = np.zeros(self.N * self.N)
+        rc = lib().orc_oc_rows(self.h, pu, rr.ctypes.data_as(ip), len(rr), out.ctypes.data_as(dp))
+        assert rc == 0, rc
         return out.reshape(self.N, self.N)
 
     def time_hessian(self, u, threads=1):

@@ -1,0 +1,157 @@
+"""The reference's own C++ tests, restated against the optimalcontrolmps
+facade (OptimalControl / ControlBasis / ControlBasisFactory / SeedGenerator)
+with the CPU restatement as TimeStepper (tests/cpp/oracle_stepper.hpp).
+
+Each test cites the reference assertion it mirrors and keeps its tolerance,
+except where the golden numbers depend on ITensor-DMRG ground states (CostTests):
+our states come from exact diagonalisation and shift the t=0 fidelity by
+<= 5.8e-6, so fidelities are checked at 1e-5 and costs at 5e-6 there.
+"""
+import numpy as np
+import pytest
+
+import facade_build as fb
+import reference_goldens as RG
+
+
+@pytest.fixture(scope="module")
+def statedir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("states")
+    fb.write_states(str(d))
+    return str(d)
+
+
+@pytest.fixture(scope="module")
+def res(statedir):
+    cache = {}
+
+    def get(scenario):
+        if scenario not in cache:
+            cache[scenario] = fb.run("oracle", scenario, statedir)
+        return cache[scenario]
+    return get
+
+
+def A(x):
+    return np.asarray(x, dtype=float)
+
+
+# ------------------------------------------------------------ ControlBasisTests
+def test_simple_matrix_basis(res):
+    r = res("basis")
+    assert np.allclose(r["simple_u_c0"], 1.0, atol=1e-8)                    # :52-58
+    assert np.allclose(r["simple_u_c1"], 1 + 2.0 * 4, atol=1e-8)            # :60-67
+    assert np.allclose(r["simple_u_cached"], r["simple_u_c1"], atol=1e-8)   # :69-74 new_control=false
+    assert np.allclose(r["simple_g0"], 0, atol=1e-8)                        # :80-87
+    assert np.allclose(r["simple_g1"], 2.0 * 5, atol=1e-8)                  # :89-96
+    assert np.allclose(r["simple_jac"], 2.0, atol=1e-8)                     # :99-113
+    assert np.allclose(r["simple_h1"], 4.0 * 25, atol=1e-8)
+
+
+def test_chopped_sine_basis_goldens(res):
+    r = res("basis")
+    assert np.allclose(r["cs_u_c0"], 1 + 0.1 * np.arange(11), atol=1e-6)   # :186-192
+    assert np.abs(A(r["cs_u_c1"]) - RG.CS_U2).max() < 5e-6                   # :194-204
+    assert np.abs(A(r["cs_u_cached"]) - A(r["cs_u_c1"])).max() < 5e-6        # :206-211
+    assert np.abs(A(r["cs_g0"])).max() < 5e-6                                # :217-224
+    assert np.abs(A(r["cs_g1"]) - RG.CS_GRADC2).max() < 5e-6                 # :226-237
+    assert np.abs(A(r["cs_jac"]) - A(RG.CS_JAC)).max() < 5e-6                # :243-268
+    assert np.abs(A(r["cs_h0"])).max() < 1e-10                               # :274-284
+    assert np.abs(A(r["cs_h1"]) - A(RG.CS_HESS_ONES)).max() < 1e-4           # :286-310
+    assert np.abs(A(r["cs_h3"]) - A(RG.CS_HESS_RAMP)).max() < 1e-4           # :312-343
+
+
+def test_seed_generator(res):
+    r = res("basis")
+    assert np.allclose(r["linspace"], np.linspace(0, 1, 11), atol=1e-12)
+    x = np.linspace(0, 100, 11)
+    assert np.allclose(r["sigmoid"], 1 / (1 + np.exp(-8.0 * (x - 1.1))), rtol=1e-12)
+    # adiabaticSeed (include/SeedGenerator.hpp:97-116), u 2 -> 50
+    xs, pp, k, a0 = 40.0, 3.5, 1.0 / 3.0, 0.01
+    exp = np.where(x < xs, (pp - 2.0 - a0 * xs) / (1 + np.exp(-k * (x - xs / 2))) + 2.0 + a0 * x,
+                   np.exp(np.log(50.0 - pp + 1) / (100 - xs) * (x - xs)) + pp - 1)
+    assert np.allclose(r["adiabatic"], exp, rtol=1e-12)
+    assert abs(r["adiabatic"][-1] - 50.0) < 1e-9
+
+
+# ------------------------------------------------------------ CostTests
+@pytest.mark.parametrize("reg", ["", "_reg"])
+def test_cost_goldens(res, reg):
+    r = res("cost")
+    tol_c = 5e-6 if not reg else 1e-1                                        # :78/:93 (1e-6), :147/:197 (1e-1)
+    if not reg:
+        assert abs(r["grape_lin_cost"] - RG.COST_LINEAR) < tol_c             # :68-84
+        assert abs(r["grape_ones_cost"] - RG.COST_ONES) < tol_c              # :86-99
+        assert abs(r["group_c0_cost"] - RG.COST_LINEAR) < tol_c              # :102-118
+        assert abs(r["group_lin_cost"] - RG.COST_GROUP_LIN) < tol_c          # :120-133
+    else:
+        assert abs(r["grape_lin_cost_reg"] - RG.COST_LINEAR_GAMMA1) < tol_c  # :136-152
+        assert abs(r["grape_ones_cost_reg"] - RG.COST_ONES) < 5e-6           # :154-167 (flat control: no reg)
+        assert abs(r["group_c0_cost_reg"] - RG.COST_LINEAR_GAMMA1) < tol_c   # :171-187
+        assert abs(r["group_lin_cost_reg"] - RG.COST_GROUP_LIN_GAMMA1) < tol_c  # :189-203
+    for key, gold in [("grape_lin_fid", RG.FID_LINEAR), ("grape_ones_fid", RG.FID_ONES),
+                      ("group_c0_fid", RG.FID_LINEAR), ("group_lin_fid", RG.FID_GROUP_LIN)]:
+        f = A(r[key + reg])
+        assert f.shape == (11,)
+        assert np.abs(f[:-1] - A(gold)[:-1]).max() < 1e-5                    # reference checks i < N-1 at 1e-6
+
+
+def test_time_axis_and_jacobian(res):
+    r = res("cost")
+    assert np.allclose(r["time_axis"], 0.01 * np.arange(11), atol=1e-12)     # getTimeAxis (:183-197)
+    assert np.array_equal(A(r["grape_jac"]), np.eye(11))                     # getControlJacobian GRAPE (:572-585)
+
+
+# ------------------------------------------------------------ GradientTests
+@pytest.mark.parametrize("mode", ["", "_bfgs"])
+def test_gradient_fd(res, mode):
+    r = res("gradient")
+    for alg, rel in [("grape", 1e-3), ("group", 2e-3)]:                      # :140-157, :186-203
+        a, n = A(r[f"{alg}_ana{mode}"]), A(r[f"{alg}_num{mode}"])
+        assert a.shape == n.shape
+        assert np.all(np.abs(a - n)[1:-1] <= np.abs(n[1:-1]) * rel + 1e-12)
+        a, n = A(r[f"{alg}_ana_reg{mode}"]), A(r[f"{alg}_num_reg{mode}"])  # gamma = 1: 1e-5 relative
+        assert np.all(np.abs(a - n)[1:-1] <= np.abs(n[1:-1]) * 1e-5 + 1e-9)
+
+
+def test_gradient_seq_vs_parallel(res):
+    r = res("gradient")                                                      # :250-285 (1e-11)
+    assert np.abs(A(r["grad_seq"]) - A(r["grad_par"]))[1:-1].max() <= 1e-11
+    assert np.abs(A(r["grad_seq_bfgs"]) - A(r["grad_par_bfgs"]))[1:-1].max() <= 1e-11
+    assert np.abs(A(r["grad_seq"]) - A(r["grad_seq_bfgs"]))[1:-1].max() <= 1e-10   # SequencingTest premise
+
+
+# ------------------------------------------------------------ HessianTests
+def test_hessian_fd(res):
+    r = res("hessian")
+    a, n = A(r["grape_ana"]), A(r["grape_num"])                              # :178-205
+    assert a.shape == (11, 11)
+    inner = (slice(1, -1), slice(1, -1))
+    assert np.all(np.abs(a - n)[inner] <= np.abs(n)[inner] * 5e-3 + 1e-9)
+    dA = A(r["grape_ana_reg"]) - a
+    dN = A(r["grape_num_reg"]) - n
+    assert np.abs(dA - dN)[inner].max() < 1e-5                                # gamma = 1 part, 1e-5 absolute
+    ga, gn = A(r["group_ana"]), A(r["group_num"])                            # :207-252
+    assert ga.shape == (8, 8)
+    # 40% relative as in the reference, plus the forward-difference truncation
+    # error eps * |d^3 J| ~ 1e-3 * 3e-5 of the eps = 1e-3 stencil as an absolute
+    # floor (entries of the smooth-basis Hessian go down to ~1e-7)
+    assert np.all(np.abs(ga - gn) <= np.abs(gn) * 0.4 + 5e-8)
+    dA = A(r["group_ana_reg"]) - ga
+    dN = A(r["group_num_reg"]) - gn
+    assert np.abs(dA - dN).max() < 1e-5
+
+
+def test_hessian_seq_vs_parallel(res):
+    r = res("hessian")                                                       # :254-269 (1e-11)
+    assert np.abs(A(r["hess_seq"]) - A(r["hess_par"]))[1:-1, 1:-1].max() <= 1e-11
+
+
+# ------------------------------------------------------------ SequencingTest
+SEQ_KEYS = ["same_CGH", "same_bfgs_CGH", "same_GCH", "same_bfgs_GCH", "same_CHG", "same_GHC", "same_HGC",
+            "same_HCG", "new_cost", "new_grad", "new_hess", "new_cost_cost", "new_grad_grad", "new_hess_hess"]
+
+
+@pytest.mark.parametrize("key", SEQ_KEYS)
+def test_sequencing(res, key):
+    assert res("sequencing")[key] is True                                    # tests/SequencingTest.cpp:81-263

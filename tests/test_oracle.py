@@ -1,0 +1,118 @@
+"""The CPU oracle (oracle/, a restatement of BH_tDMRG + OptimalControl) pinned
+against (1) the committed fixtures it produced (regression), (2) an
+independent exact state-vector implementation of the same Trotter scheme
+(numpy, full Hilbert space), and (3) its building blocks
+(Hermitian eigensolver, ITensor truncation rule).  The reference's own golden
+numbers are checked through the facade in test_facade_cpu.py.
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from conftest import state_key
+from optimalcontrolmps_amd import ed
+
+CASES = [  # fixture name, (L, p, N, J), U_init, U_target, dt, cutoff, maxm
+    ("grad_L5p6", (5, 6, 5, 1.0), 2.0, 12.0, 0.01, 1e-8, 0),
+    ("hess_L5p6", (5, 6, 5, 1.0), 2.0, 12.0, 0.01, 1e-8, 0),
+    ("seq_L3p4", (3, 4, 3, 2.0), 2.0, 12.0, 0.01, 1e-7, 0),
+    ("even_L4p3", (4, 3, 4, 1.0), 2.0, 10.0, 0.01, 1e-8, 0),
+]
+
+
+def orc_state(states, L, p, N, J, U):
+    k = state_key(L, p, N, J, U)
+    return O.MPS(L, p, N, states[k + "/dims"], states[k + "/data"])
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_oracle_reproduces_fixtures(states, oracle_golden, case):
+    name, (L, p, N, J), Ui, Uf, dt, cut, maxm = case
+    u = oracle_golden[name + "/u"]
+    oc = O.OC(O.Stepper(L, p, N, J, dt, cut, maxm or 5000), orc_state(states, L, p, N, J, Uf),
+              orc_state(states, L, p, N, J, Ui), len(u), 0.0)
+    g = oc.gradient(u)
+    assert np.abs(g - oracle_golden[name + "/grad"]).max() <= 1e-12
+    H = oc.hessian(u, 4)
+    Hg = oracle_golden[name + "/hess"]
+    assert np.abs(H - Hg).max() <= 1e-12 * np.abs(Hg).max()
+    assert list(oc.state(0, len(u) - 1).bond_dims()) == list(oracle_golden[name + "/psiT_dims"])
+
+
+def test_oracle_config1_gradient_fixture(states, oracle_golden):
+    u = oracle_golden["config1/u"]
+    oc = O.OC(O.Stepper(5, 5, 5, 1.0, 0.01, 1e-8, 80), orc_state(states, 5, 5, 5, 1.0, 50.0),
+              orc_state(states, 5, 5, 5, 1.0, 2.5), len(u), 0.0)
+    assert np.abs(oc.gradient(u) - oracle_golden["config1/grad"]).max() <= 1e-12
+    assert list(oc.state(0, len(u) - 1).bond_dims()) == list(oracle_golden["config1/psiT_dims"])
+
+
+def exact_gradient(L, p, Q, J, dt, u, ini, tgt):
+    """GRAPE gradient from full state vectors: calcPsi/calcXi/calcDivT
+    (src/OptimalControl.cpp:375-419) and g_i = dt Re(divT_i F i) (:240-246)."""
+    N = len(u)
+    psi = [ini]
+    for i in range(N - 1):
+        psi.append(ed.exact_step(psi[-1], L, p, J, dt, u[i], u[i + 1], True))
+    xi = [None] * N
+    xi[N - 1] = tgt
+    for i in range(N - 1, 0, -1):
+        xi[i - 1] = ed.exact_step(xi[i], L, p, J, dt, u[i], u[i - 1], False)
+    dH = ed.dH_full(L, p)
+    divT = np.array([np.vdot(xi[i], dH * psi[i]) for i in range(N)])
+    F = np.vdot(psi[-1], tgt)
+    return dt * (divT * F * 1j).real, divT, F
+
+
+@pytest.mark.parametrize("L,p,Q,J,Ui,Uf", [(3, 4, 3, 2.0, 2.0, 12.0), (4, 3, 4, 1.0, 2.0, 10.0),
+                                            (5, 6, 5, 1.0, 2.0, 12.0)])
+def test_oracle_gradient_matches_exact_state_vector(states, L, p, Q, J, Ui, Uf):
+    dt = 0.01
+    u = np.random.default_rng(L * 10 + p).uniform(2, 10, 12)
+    ini_m, tgt_m = orc_state(states, L, p, Q, J, Ui), orc_state(states, L, p, Q, J, Uf)
+    full = lambda m: ed.full_from_mps(m.dims, m.data, L, p, Q)
+    g_ex, divT_ex, F_ex = exact_gradient(L, p, Q, J, dt, u, full(ini_m), full(tgt_m))
+    # cutoff 1e-14 (the gauge-move cutoff too) discards Schmidt weight < 1e-14
+    # per decomposition, i.e. amplitude errors up to ~1e-7 per step
+    oc = O.OC(O.Stepper(L, p, Q, J, dt, 1e-14), tgt_m, ini_m, len(u), 0.0)
+    g = oc.gradient(u)
+    divT, F = oc.divT_F()
+    assert abs(F - F_ex) < 1e-8
+    assert np.abs(divT - divT_ex).max() < 1e-7
+    assert np.abs(g - g_ex).max() < 1e-9
+
+
+def test_oracle_step_matches_exact_trotter_step(states):
+    L, p, Q, J = 5, 6, 5, 1.0
+    m = orc_state(states, L, p, Q, J, 2.0)
+    st = O.Stepper(L, p, Q, J, 0.01, 1e-14)
+    v = ed.full_from_mps(m.dims, m.data, L, p, Q)
+    for fwd in (True, False):
+        out = st.step(m, 3.0, 7.0, fwd)
+        w = ed.full_from_mps(out.dims, out.data, L, p, Q)
+        ref = ed.exact_step(v, L, p, J, 0.01, 3.0, 7.0, fwd)
+        assert abs(abs(np.vdot(ref, w)) - 1.0) < 1e-12
+        assert np.abs(w - ref * np.vdot(ref, w)).max() < 1e-9
+
+
+def test_oracle_heev_matches_numpy():
+    rng = np.random.default_rng(0)
+    for n in (1, 2, 5, 17):
+        A = rng.normal(size=(n, n)) + 1j * rng.normal(size=(n, n))
+        A = A @ A.conj().T
+        w, V = O.heev(A)
+        assert np.allclose(np.sort(w), np.linalg.eigvalsh(A), atol=1e-12 * np.abs(w).max())
+        assert np.allclose(A @ V, V * w, atol=1e-11 * np.abs(w).max())
+        assert np.allclose(V.conj().T @ V, np.eye(n), atol=1e-12)
+
+
+def test_truncation_rule():
+    # discard smallest weights while the discarded sum stays < cutoff * total; Maxm cap; Minm = 1
+    P = np.array([0.5, 0.3, 0.15, 0.04, 0.009, 0.001])
+    assert O.truncate(P, 0.0, 100) == 6
+    assert O.truncate(P, 0.002, 100) == 5
+    assert O.truncate(P, 0.0101, 100) == 4
+    assert O.truncate(P, 0.06, 100) == 3
+    assert O.truncate(P, 0.06, 2) == 2
+    assert O.truncate(P, 0.99, 100) == 1
+    assert O.truncate(np.array([1.0]), 0.5, 100) == 1
