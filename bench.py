@@ -141,7 +141,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": measured_traffic("k_hessian_rows"),
                 "alg_bytes_per_launch": bytes_per_launch,
                 "fp64_achieved_tflops": flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0,
                 "fp64_peak_tflops": FP64_PEAK_TFS,
@@ -153,6 +153,17 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def measured_traffic(kernel, tag="r01"):
+    """HBM bytes per dispatch of `kernel` from the committed rocprofv3 PMC passes
+    of this same command (profiles/<tag>_summary.json, written by
+    tools/prof_summary.py; FETCH_SIZE doubled per the gfx950 calibration)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"{tag}_summary.json")) as f:
+            return json.load(f)["pmc_per_dispatch"][kernel]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(ini, tgt, u, threads):

@@ -56,6 +56,8 @@ typedef struct ocg_info {
  * dH = sum_k 0.5 n_k(n_k-1) MPO data (:10-14) on `device`. */
 int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm,
                ocg_ctx** out);
+/* number of visible HIP devices (OCG_EHIP and *n = 0 without a GPU) */
+int ocg_device_count(int* n);
 int ocg_destroy(ocg_ctx* ctx);
 /* last error message of ctx (or of the last failed ocg_create when ctx == NULL) */
 const char* ocg_last_error(const ocg_ctx* ctx);

@@ -315,6 +315,18 @@ size_t ocg_mps_nelem(int L, int p, int Q, const int* dims) {
   return s;
 }
 
+int ocg_device_count(int* n) {
+  if (!n) return OCG_EINVAL;
+  *n = 0;
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess || *n <= 0) {
+    g_create_error = std::string("no HIP device available: ") + hipGetErrorString(e);
+    *n = 0;
+    return OCG_EHIP;
+  }
+  return OCG_OK;
+}
+
 int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm, ocg_ctx** out) {
   if (!out) { g_create_error = "out is NULL"; return OCG_EINVAL; }
   *out = nullptr;

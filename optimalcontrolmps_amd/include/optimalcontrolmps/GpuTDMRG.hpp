@@ -150,10 +150,13 @@ class GpuTDMRG::Engine {
   void setShards(size_t n) {
     if (n < 1) throw std::invalid_argument("Mininum threadCount is 1.");
     while (shards.size() > n) shards.pop_back();
+    int ndev = 0;
+    detail::check(ocg_device_count(&ndev), nullptr, "ocg_device_count");
     while (shards.size() < n) {
-      const int s = int(shards.size());
-      detail::CtxPtr c = detail::make_ctx(stepper.device + s, stepper.L, stepper.p, tgt.Q, stepper.J, stepper.tstep,
-                                          stepper.args);
+      // shard s on device (first + s) mod #devices: more shards than GPUs run
+      // concurrently on separate streams of the same device
+      const int dev = (stepper.device + int(shards.size())) % ndev;
+      detail::CtxPtr c = detail::make_ctx(dev, stepper.L, stepper.p, tgt.Q, stepper.J, stepper.tstep, stepper.args);
       detail::check(ocg_set_states(c.get(), tgt.dims.data(), tgt.raw(), ini.dims.data(), ini.raw()), c.get(),
                     "ocg_set_states");
       shards.push_back(std::move(c));

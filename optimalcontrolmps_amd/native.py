@@ -66,6 +66,7 @@ SIGNATURES = [
     ("ocg_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
                              C.POINTER(C.c_void_p)]),
     ("ocg_destroy", C.c_int, [C.c_void_p]),
+    ("ocg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("ocg_last_error", C.c_char_p, [C.c_void_p]),
     ("ocg_get_info", C.c_int, [C.c_void_p, C.POINTER(OcgInfo)]),
     ("ocg_set_tstep", C.c_int, [C.c_void_p, C.c_double]),

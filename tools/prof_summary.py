@@ -1,0 +1,78 @@
+"""Summarise rocprofv3 rocpd databases into the committed profiles/ files.
+
+  python tools/prof_summary.py <tag>
+reads gpurun_out/prof_<tag>/run_results.db (--kernel-trace --stats) and the
+two PMC passes gpurun_out/pmc_{fetch,write}_<tag>/run_results.db, writes
+profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.csv and
+profiles/<tag>_summary.json (per-launch HBM traffic of each kernel, with the
+gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE counts
+half the bytes of 16-B-per-lane reads, so it is doubled; WRITE_SIZE as is).
+"""
+import csv
+import json
+import os
+import sqlite3
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0]
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    # rocpd top_kernels durations are in microseconds
+    return [dict(kernel=short(r[0]), calls=r[1], total_ms=r[2] / 1e3, avg_ms=r[3] / 1e3, pct=r[4]) for r in rows]
+
+
+def pmc(db, counter):
+    c = sqlite3.connect(db)
+    out = {}
+    for name, val in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
+                               (counter,)):
+        k = short(name)
+        s = out.setdefault(k, [0.0, 0])
+        s[0] += val
+        s[1] += 1
+    return out
+
+
+def main(tag):
+    g = os.path.join(ROOT, "gpurun_out")
+    ks = kernel_stats(os.path.join(g, f"prof_{tag}", "run_results.db"))
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["kernel", "calls", "total_ms", "avg_ms", "pct"])
+        w.writeheader()
+        for r in ks:
+            w.writerow(r)
+    fetch = pmc(os.path.join(g, f"pmc_fetch_{tag}", "run_results.db"), "FETCH_SIZE")
+    write = pmc(os.path.join(g, f"pmc_write_{tag}", "run_results.db"), "WRITE_SIZE")
+    per = {}
+    with open(os.path.join(prof, f"{tag}_pmc.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "dispatches", "FETCH_SIZE_KB_per_dispatch", "WRITE_SIZE_KB_per_dispatch",
+                    "hbm_bytes_per_dispatch_corrected"])
+        for k in sorted(set(fetch) | set(write)):
+            fk = fetch.get(k, [0.0, 1])
+            wk = write.get(k, [0.0, 1])
+            f_kb, w_kb = fk[0] / fk[1], wk[0] / wk[1]
+            corrected = 2.0 * f_kb * 1024 + w_kb * 1024
+            per[k] = dict(dispatches=fk[1], fetch_kb=f_kb, write_kb=w_kb, hbm_bytes=corrected)
+            w.writerow([k, fk[1], f"{f_kb:.3f}", f"{w_kb:.3f}", f"{corrected:.0f}"])
+    summary = dict(tag=tag, kernels=ks, pmc_per_dispatch=per,
+                   note="rocprofv3 --kernel-trace --stats and separate --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                        "`python3 bench.py` (config 1); FETCH_SIZE doubled per the gfx950 calibration")
+    with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: v for k, v in per.items() if k.startswith("k_")}, indent=1))
+    for r in ks[:4]:
+        print(r)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
