@@ -11,7 +11,9 @@
 //  path (optimalcontrolmps_amd/) never links or calls it.
 //
 //  Reference citations are path:line relative to the reference repository.
-//  Parity pins: tests/test_oracle_golden.py (CostTests golden fidelities,
+//  Parity pins: tests/test_oracle.py (fixtures, exact state-vector
+//  cross-check, eigensolver, truncation rule) and tests/test_facade_cpu.py
+//  (the reference tests restated: CostTests golden fidelities,
 //  FD gradient/Hessian properties, sequencing semantics, exact state-vector
 //  cross-check).  ITensor internals that no reference test pins (truncation
 //  scale, gauge-move and exactApplyMPO compression rules) are fixed here
