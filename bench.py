@@ -69,12 +69,11 @@ def main():
     Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=dev)
 
     def one_step():
-        eng.propagate(u, 3)                      # calcPsi + calcXi (two chains)
-        divT = eng.div_t()                       # calcDivT
-        F = eng.overlap_factor()                 # overlapFactor
+        # fused getHessian: psi/xi chains, xiHlist and this rank's rows in one
+        # pipelined launch (rows start as their psi_i appears), then divT, F
+        # and the batched <xiH_j|psiH> overlaps (ocg_hessian)
+        H, divT, F = eng.hessian(u, rows)
         g = dt * (divT * F * 1j).real            # calcFidelityGrad (gamma = 0)
-        eng.xi_dH()                              # xiHlist
-        H = eng.hessian_rows(u, rows, F, divT)   # calcHessianRow for this rank's rows
         if world > 1:
             Hdev.copy_(torch.from_numpy(H))
             dist.reduce(Hdev, dst=0)             # RCCL sum of disjoint row entries
@@ -101,7 +100,8 @@ def main():
 
     rows_total = (Nt - 2) * args.steps
     value = rows_total / elapsed
-    st_rows = eng.stats(3)
+    st_rows = eng.stats(5)       # k_pipeline: trajectories + row re-propagation (dominant)
+    st_ovl = eng.stats(6)        # k_row_overlaps
     st_traj = eng.stats(0)
     row_steps = (Nt - 2) * (Nt - 3) // 2
     sweep_steps = args.steps * (2 * (Nt - 1) * world + row_steps)
@@ -129,19 +129,18 @@ def main():
                        "rows_per_step": Nt - 2, "parallelism": f"rows sharded zig-zag over {world} GPU(s)"},
             "sweep_steps_per_sec": sweep_steps / elapsed,
             "kernels": {
-                "hessian_rows": {"avg_ms": launch_ms, "launches": st_rows["launches"]},
-                "trajectory": {"avg_ms": st_traj["ms"] / max(1, st_traj["launches"])},
-                "overlaps_ms": eng.stats(1)["ms"] / max(1, args.steps),
-                "apply_dH_ms": eng.stats(2)["ms"] / max(1, args.steps),
+                "pipeline": {"avg_ms": launch_ms, "launches": st_rows["launches"]},
+                "row_overlaps": {"avg_ms": st_ovl["ms"] / max(1, st_ovl["launches"]), "launches": st_ovl["launches"]},
+                "divT_F_overlaps_ms": eng.stats(1)["ms"] / max(1, args.steps),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_hessian_rows",
+                "kernel": "k_pipeline",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": measured_traffic("k_hessian_rows"),
+                "traffic": measured_traffic("k_pipeline"),
                 "alg_bytes_per_launch": bytes_per_launch,
                 "fp64_achieved_tflops": flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0,
                 "fp64_peak_tflops": FP64_PEAK_TFS,

@@ -109,13 +109,25 @@ int ocg_xi_dH(ocg_ctx* ctx);
  * Hessian is the caller's.  Requires ocg_propagate(..,3) + ocg_xi_dH. */
 int ocg_hessian_rows(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows, const double* F,
                      const double* divT, double* H);
+/* One full getHessian(u, new_control = true) fidelity part, fused
+ * (calcHessian_parallel, src/OptimalControl.cpp:281-338, without the
+ * regularisation Hessian, which is the caller's): psi_t and xi_t, xiHlist,
+ * divT, F and the rows[0..nrows-1] (each in 1..N-2).  Rows start as soon as
+ * their psi_i is available and the <xiH_j|psiH> overlaps run as one batched
+ * launch afterwards; arithmetic per row is that of ocg_hessian_rows.  H is
+ * row-major N x N, caller-zeroed (rows' entries and mirrors written); divT
+ * (2N doubles) and F (2) are returned for the gradient.  Leaves the same
+ * device state as ocg_propagate(..,3) + ocg_xi_dH. */
+int ocg_hessian(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                double* F);
 /* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host */
 int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
 
 /* ------------------------------------------------------ instrumentation
  * Per-kernel HIP-event timing on the context's stream and the algorithmic
  * traffic model of DESIGN.md §Roofline.  kind: 0 trajectory, 1 overlaps,
- * 2 dH apply, 3 Hessian rows, 4 steps.  Sums since the last reset. */
+ * 2 dH apply, 3 Hessian rows, 4 steps, 5 fused pipeline (ocg_hessian phase 1),
+ * 6 batched row overlaps (ocg_hessian phase 2).  Sums since the last reset. */
 int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
                      double* alg_flops, long* sweep_steps);
 int ocg_reset_stats(ocg_ctx* ctx);

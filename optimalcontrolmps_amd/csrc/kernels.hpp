@@ -138,6 +138,133 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
   flush_stats(c, stats, bytes, flops, double(N - 2 - i > 0 ? N - 2 - i : 0));
 }
 
+// --------------------------------------------------------------------------
+// Fused getHessian pipeline (ocg_hessian).  Rows start as soon as their psi_i
+// exists instead of after both trajectory sweeps, and the <xiH_j|psiH_i(j)>
+// overlaps move to a second, fully parallel kernel:
+//   k_pipeline   grid [0] psi chain, [1] xi chain (each publishes state t via
+//                flags[t] / flags[N+t]), [2, 2+N) xiH_t = dH xi_t,
+//                [2+N, 2+N+nrows) row r: wait psi_i, psiH = dH psi_i, store
+//                psiH_i(i..N-2) (the states calcHessianRow overlaps, :251-279)
+//   k_row_overlaps  one workgroup per stored psiH_i(j): overlap with xiH_j, H_ij
+// Producers and consumers live in one grid; consumers only ever wait on
+// blocks 0 and 1, which are dispatched first, so progress does not depend on
+// co-residency.  A watchdog (~2 s) aborts waits and flags err.
+__device__ __forceinline__ void publish_flag(int* flag, int epoch) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int NT>
+__device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, int* err) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    long spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins > (1L << 23) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ok = 0;
+        atomicOr(err, 2);
+        break;
+      }
+    }
+    c.ISCAL[15] = ok;
+  }
+  __syncthreads();
+  const int ok = c.ISCAL[15];
+  __syncthreads();
+  return ok != 0;
+}
+
+template <int NT>
+__device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
+                                         Pool pool, int slot_init, int slot_target, int psi_base, int xi_base,
+                                         int xih_base, const double* u, int N, const int* rows, int nrows,
+                                         const int* rbase, Pool rs, double* rnorm, int* flags, int epoch, int* err,
+                                         double* stats) {
+  Chain<NT> c(P, smem);
+  c.load_tables(gf, gb, md);
+  const int b = blockIdx.x;
+  double bytes = 0, flops = 0, nsteps = 0;
+  if (b < 2) {
+    // calcPsi / calcXi (src/OptimalControl.cpp:375-407), every state published
+    const int fwd = (b == 0) ? 1 : 0;
+    const int base = fwd ? psi_base : xi_base;
+    int* fl = flags + (fwd ? 0 : N);
+    const int src = fwd ? slot_init : slot_target;
+    c.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
+    int t = fwd ? 0 : N - 1;
+    c.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
+    publish_flag(fl + t, epoch);
+    for (int s = 0; s + 1 < N; ++s) {
+      const int tn = fwd ? t + 1 : t - 1;
+      c.step(u[t], u[tn], fwd);
+      c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
+      publish_flag(fl + tn, epoch);
+      t = tn;
+    }
+    nsteps = N - 1;
+  } else if (b < 2 + N) {
+    // xiHlist[t] = exactApplyMPO(propDeriv, xi_t[t]) (:300-303)
+    const int t = b - 2;
+    if (!await_flag(c, flags + N + t, epoch, err)) return;
+    c.load(SLOT_D(pool, P, xi_base + t), SLOT_X(pool, P, xi_base + t));
+    c.apply_dH();
+    c.store(SLOT_D(pool, P, xih_base + t), SLOT_X(pool, P, xih_base + t));
+  } else {
+    const int r = b - 2 - N;
+    if (r >= nrows) return;
+    const int i = rows[r];
+    if (!await_flag(c, flags + i, epoch, err)) return;
+    // psiH = exactApplyMPO(propDeriv, psi_t[i]); normiH = norm(psiH) (:256-257)
+    c.load(SLOT_D(pool, P, psi_base + i), SLOT_X(pool, P, psi_base + i));
+    c.apply_dH();
+    const double n2 = c.site_norm2(1);
+    if (threadIdx.x == 0) rnorm[r] = sqrt(n2);
+    int k = rbase[r];
+    c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
+    for (int j = i + 1; j + 1 < N; ++j) {  // timeStepper.step(psiH, u[j-1], u[j]) (:269)
+      c.step(u[j - 1], u[j], 1);
+      ++k;
+      c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
+    }
+    nsteps = N - 2 - i;
+  }
+  c.model_totals(bytes, flops);
+  flush_stats(c, stats, bytes, flops, nsteps);
+}
+
+// H_ij from the stored psiH_i(j) (calcHessianRow's two terms, :259-277)
+template <int NT>
+__device__ OCG_INLINE void body_row_overlaps(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
+                                             Pool pool, int xih_base, const int* rows, int nrows, const int* rbase,
+                                             Pool rs, const double* rnorm, const zc* divT, const zc* Fp, int N,
+                                             double* H, double* stats) {
+  Chain<NT> c(P, smem);
+  c.load_tables(gf, gb, md);
+  const int g = blockIdx.x;
+  if (g >= rbase[nrows]) return;
+  int lo = 0, hi = nrows - 1;  // row r with rbase[r] <= g < rbase[r+1]
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rbase[mid] <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  const int r = lo, i = rows[r], j = i + (g - rbase[r]);
+  c.load(SLOT_D(rs, P, g), SLOT_X(rs, P, g));
+  const zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
+  const double b = 32.0 * c.mps_used();
+  if (threadIdx.x == 0) {
+    const zc F = *Fp, di = divT[i], dj = divT[j];
+    const double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? rnorm[r] : 1.0);  // Re(F <xiH_j|psiH> normiH)
+    const double v2 = -(di.x * dj.x + di.y * dj.y);                          // -Re(divT_i conj(divT_j))
+    const double res = P.dt * P.dt * (v1 + v2);
+    H[(size_t)i * N + j] = res;
+    if (j > i) H[(size_t)j * N + i] = res;
+  }
+  flush_stats(c, stats, b, 8.0 * b / 16.0 * 4.0, 0.0);
+}
+
 // nsteps steps per state; u holds nsteps+1 controls per state (u_stride apart)
 template <int NT>
 __device__ OCG_INLINE void body_steps(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,

@@ -65,6 +65,25 @@ __global__ __launch_bounds__(NT) void k_hessian_rows(OcgParams P, const zc* gf, 
                              stats);
 }
 
+__global__ __launch_bounds__(NT) void k_pipeline(OcgParams P, const zc* gf, const zc* gb, const int* md, Pool pool,
+                                                 int slot_init, int slot_target, int psi_base, int xi_base,
+                                                 int xih_base, const double* u, int N, const int* rows, int nrows,
+                                                 const int* rbase, Pool rs, double* rnorm, int* flags, int epoch,
+                                                 int* err, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_pipeline<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, xih_base, u, N, rows,
+                         nrows, rbase, rs, rnorm, flags, epoch, err, stats);
+}
+
+__global__ __launch_bounds__(NT) void k_row_overlaps(OcgParams P, const zc* gf, const zc* gb, const int* md,
+                                                     Pool pool, int xih_base, const int* rows, int nrows,
+                                                     const int* rbase, Pool rs, const double* rnorm,
+                                                     const zc* divT, const zc* F, int N, double* H, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_row_overlaps<NT>(smem, P, gf, gb, md, pool, xih_base, rows, nrows, rbase, rs, rnorm, divT, F, N, H,
+                             stats);
+}
+
 __global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                               Pool pool, const int* slots, int n, const double* u, int u_stride,
                                               int nsteps, int forward, double* stats) {
@@ -99,7 +118,7 @@ struct ocg_ctx {
   int* d_md = nullptr;
   Pool pool{nullptr, nullptr};
   int nslots = 0;
-  double* d_stats = nullptr;  // [5][3]
+  double* d_stats = nullptr;  // [8][3]
   int* d_idx = nullptr;       // index scratch
   int idx_cap = 0;
   double* d_u = nullptr;
@@ -109,14 +128,28 @@ struct ocg_ctx {
   double* d_H = nullptr;
   size_t H_cap = 0;
   double* d_norms = nullptr;
+  int norms_cap = 0;
   double* d_rnorm = nullptr;  // psiH norms (by row index)
   int rnorm_cap = 0;
   int* d_idx2 = nullptr;      // index scratch of the psiH launch
   int idx2_cap = 0;
+  // fused pipeline (ocg_hessian)
+  Pool rs{nullptr, nullptr};  // stored psiH_i(j) states
+  size_t rs_cap = 0;
+  int* d_flags = nullptr;     // [2N] psi / xi publication epochs
+  int flags_cap = 0;
+  int epoch = 0;
+  int* d_err = nullptr;
+  int* d_rows = nullptr;      // rows, then rbase (nrows + 1)
+  int rows_cap = 0;
+  zc* d_pc = nullptr;         // divT (N) and F (1) on the device
+  int pc_cap = 0;
+  double* d_prn = nullptr;    // psiH norms by row slot
+  int prn_cap = 0;
   // trajectory state
   int N = 0;
   bool have_states = false, have_psi = false, have_xi = false, have_xih = false;
-  KStat kst[5];
+  KStat kst[8];
   // slot map
   int slot_init() const { return 0; }
   int slot_target() const { return 1; }
@@ -284,6 +317,8 @@ static int set_lds(ocg_ctx* c) {
   HIPCHK(c, hipFuncSetAttribute((const void*)k_apply_dH, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIPCHK(c, hipFuncSetAttribute((const void*)k_hessian_rows, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIPCHK(c, hipFuncSetAttribute((const void*)k_steps, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_pipeline, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_row_overlaps, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   return 0;
 }
 
@@ -358,8 +393,9 @@ int ocg_create(int device, int L, int p, int npart, double J, double tstep, doub
   }
   if (hipMalloc(&c->d_md, sizeof(int) * c->md.size()) != hipSuccess ||
       hipMemcpy(c->d_md, c->md.data(), sizeof(int) * c->md.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMalloc(&c->d_stats, sizeof(double) * 15) != hipSuccess ||
-      hipMemset(c->d_stats, 0, sizeof(double) * 15) != hipSuccess) {
+      hipMalloc(&c->d_stats, sizeof(double) * 24) != hipSuccess ||
+      hipMemset(c->d_stats, 0, sizeof(double) * 24) != hipSuccess ||
+      hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess) {
     c->err = "device allocation failed";
     return bail(OCG_EHIP);
   }
@@ -378,6 +414,13 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->pool.dims) (void)hipFree(c->pool.dims);
   if (c->pool.data) (void)hipFree(c->pool.data);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->rs.dims) (void)hipFree(c->rs.dims);
+  if (c->rs.data) (void)hipFree(c->rs.data);
+  if (c->d_flags) (void)hipFree(c->d_flags);
+  if (c->d_err) (void)hipFree(c->d_err);
+  if (c->d_rows) (void)hipFree(c->d_rows);
+  if (c->d_pc) (void)hipFree(c->d_pc);
+  if (c->d_prn) (void)hipFree(c->d_prn);
   if (c->d_idx) (void)hipFree(c->d_idx);
   if (c->d_u) (void)hipFree(c->d_u);
   if (c->d_c) (void)hipFree(c->d_c);
@@ -475,14 +518,8 @@ static int launch_apply_dH(ocg_ctx* c, const std::vector<int>& in, const std::ve
   const OcgParams& P = c->P;
   int n = int(in.size());
   if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * n)) return rc;
-  int ncap = 0;
-  if (norms) {
-    if (c->d_norms) (void)hipFree(c->d_norms);
-  if (c->d_rnorm) (void)hipFree(c->d_rnorm);
-  if (c->d_idx2) (void)hipFree(c->d_idx2);
-    c->d_norms = nullptr;
-    if (int rc = ensure_buf(c, c->d_norms, ncap, n)) return rc;
-  }
+  if (norms)
+    if (int rc = ensure_buf(c, c->d_norms, c->norms_cap, n)) return rc;
   std::vector<int> idx(in);
   idx.insert(idx.end(), outs.begin(), outs.end());
   HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
@@ -645,6 +682,112 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
   return 0;
 }
 
+int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                double* F) {
+  if (!c || !u || !H || !divT || !F || (nrows > 0 && !rows) || nrows < 0 || N < 4)
+    return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
+  for (int r = 0; r < nrows; ++r)
+    if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
+  HIPCHK(c, hipSetDevice(c->device));
+  const OcgParams& P = c->P;
+  if (N != c->N) {
+    c->N = N;
+    c->have_psi = c->have_xi = c->have_xih = false;
+  }
+  if (int rc = ensure_slots(c, 6 + 4 * N)) return rc;
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, N)) return rc;
+  if (int rc = ensure_buf(c, c->d_pc, c->pc_cap, N + 1)) return rc;
+  if (int rc = ensure_buf(c, c->d_rows, c->rows_cap, 2 * nrows + 2)) return rc;
+  if (int rc = ensure_buf(c, c->d_prn, c->prn_cap, nrows + 1)) return rc;
+  if (2 * N > c->flags_cap) {  // publication flags start at 0 (< any epoch)
+    if (c->d_flags) (void)hipFree(c->d_flags);
+    c->d_flags = nullptr;
+    c->flags_cap = 0;
+    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N)) return rc;
+    HIPCHK(c, hipMemset(c->d_flags, 0, sizeof(int) * c->flags_cap));
+    c->epoch = 0;
+  }
+  // stored row states: row i keeps psiH_i(j), j = i..N-2
+  std::vector<int> rb(2 * nrows + 1);  // rows[0..nrows) then rbase[0..nrows]
+  size_t total = 0;
+  for (int r = 0; r < nrows; ++r) rb[r] = rows[r];
+  for (int r = 0; r < nrows; ++r) {
+    rb[nrows + r] = int(total);
+    total += size_t(N - 1 - rows[r]);
+  }
+  rb[2 * nrows] = int(total);
+  if (total > c->rs_cap) {
+    if (c->rs.dims) (void)hipFree(c->rs.dims);
+    if (c->rs.data) (void)hipFree(c->rs.data);
+    c->rs = Pool{nullptr, nullptr};
+    c->rs_cap = 0;
+    HIPCHK(c, hipMalloc(&c->rs.dims, sizeof(int) * total * P.nsq));
+    HIPCHK(c, hipMalloc(&c->rs.data, sizeof(zc) * total * P.cap));
+    c->rs_cap = total;
+  }
+  size_t hn = size_t(N) * N;
+  if (hn > c->H_cap) {
+    if (c->d_H) (void)hipFree(c->d_H);
+    HIPCHK(c, hipMalloc(&c->d_H, sizeof(double) * hn));
+    c->H_cap = hn;
+  }
+  const int epoch = ++c->epoch;
+  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_rows, rb.data(), sizeof(int) * rb.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
+  const int* d_rows = c->d_rows;
+  const int* d_rbase = c->d_rows + nrows;
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_pipeline, dim3(2 + N + nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb,
+                     c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->xih_base(),
+                     c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err,
+                     c->d_stats + 5 * 3);
+  if (int rc = end_kernel(c, 5)) return rc;
+  int err = 0;
+  HIPCHK(c, hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) return fail(c, OCG_ENUM, "pipeline watchdog: a consumer timed out waiting for a trajectory state");
+  c->have_psi = c->have_xi = c->have_xih = true;
+  // divT_i = <xi_i|dH|psi_i> and F = <psi_{N-1}|target> into d_pc (device-resident)
+  {
+    std::vector<int> idx(2 * N + 2);
+    for (int i = 0; i < N; ++i) { idx[i] = c->xi_base() + i; idx[N + i] = c->psi_base() + i; }
+    idx[2 * N] = c->psi_base() + N - 1;
+    idx[2 * N + 1] = c->slot_target();
+    if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * N + 2)) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
+    if (int rc = begin_kernel(c)) return rc;
+    hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+                       c->d_idx, c->d_idx + N, N, 1, c->d_pc, c->d_stats + 1 * 3);
+    hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+                       c->d_idx + 2 * N, c->d_idx + 2 * N + 1, 1, 0, c->d_pc + N, c->d_stats + 1 * 3);
+    if (int rc = end_kernel(c, 1)) return rc;
+  }
+  if (total > 0) {
+    if (int rc = begin_kernel(c)) return rc;
+    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb,
+                       c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
+                       c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
+    if (int rc = end_kernel(c, 6)) return rc;
+  }
+  std::vector<zc> pc(N + 1);
+  HIPCHK(c, hipMemcpy(pc.data(), c->d_pc, sizeof(zc) * (N + 1), hipMemcpyDeviceToHost));
+  for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
+  F[0] = pc[N].x;
+  F[1] = pc[N].y;
+  std::vector<double> h(hn);
+  HIPCHK(c, hipMemcpy(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost));
+  for (int r = 0; r < nrows; ++r) {
+    const int i = rows[r];
+    for (int j = i; j + 1 < N; ++j) {
+      H[size_t(i) * N + j] = h[size_t(i) * N + j];
+      H[size_t(j) * N + i] = h[size_t(j) * N + i];
+    }
+  }
+  return 0;
+}
+
 int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t cap, size_t* nelem) {
   if (!c || !dims || !data) return OCG_EINVAL;
   if (t < 0 || t >= c->N) return fail(c, OCG_EINVAL, "t out of range");
@@ -657,7 +800,7 @@ int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t 
 
 int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, double* alg_bytes, double* alg_flops,
                      long* sweep_steps) {
-  if (!c || kind < 0 || kind > 4) return OCG_EINVAL;
+  if (!c || kind < 0 || kind > 6) return OCG_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
   double s[3];
   HIPCHK(c, hipMemcpy(s, c->d_stats + 3 * kind, sizeof(s), hipMemcpyDeviceToHost));
@@ -689,7 +832,7 @@ int ocg_profile(ocg_ctx* c, double* out32, int reset) {
 int ocg_reset_stats(ocg_ctx* c) {
   if (!c) return OCG_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemset(c->d_stats, 0, sizeof(double) * 15));
+  HIPCHK(c, hipMemset(c->d_stats, 0, sizeof(double) * 24));
   for (auto& k : c->kst) k = KStat{};
   return 0;
 }

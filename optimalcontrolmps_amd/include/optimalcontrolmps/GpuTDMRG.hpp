@@ -218,6 +218,41 @@ class GpuTDMRG::Engine {
       for (size_t i = 0; i < N; ++i)
         for (size_t j = 0; j < N; ++j) H[i][j] += part[s][i * N + j];
   }
+  // getHessian(u, new_control = true) fidelity part in one pipelined call per
+  // shard (ocg_hessian): trajectories, xiHlist and the shard's rows overlap
+  void hessianFresh(const stdvec& u, Cplx& F, std::vector<Cplx>& dT, rowmat& H) {
+    check_len(u);
+    const size_t G = shards.size();
+    std::vector<std::vector<int>> rows(G);
+    for (size_t i = 1, k = 0; i + 1 < N; ++i, ++k) {
+      const size_t r = k % (2 * G);
+      rows[r < G ? r : 2 * G - 1 - r].push_back(int(i));
+    }
+    std::vector<std::vector<double>> part(G, std::vector<double>(N * N, 0.0));
+    std::vector<double> dv(2 * N);
+    double Fv[2] = {0, 0};
+    on_all_indexed([&](size_t s, ocg_ctx* c) {
+      std::vector<double> dvs(2 * N);
+      double Fs[2];
+      detail::check(ocg_hessian(c, u.data(), int(N), rows[s].data(), int(rows[s].size()), part[s].data(), dvs.data(),
+                                Fs),
+                    c, "ocg_hessian");
+      if (s == 0) {
+        dv = dvs;
+        Fv[0] = Fs[0];
+        Fv[1] = Fs[1];
+      }
+    });
+    for (size_t s = 0; s < G; ++s) fresh[s] = 0;
+    u_psi = u;
+    u_xi = u;
+    F = Cplx(Fv[0], Fv[1]);
+    dT.resize(N);
+    for (size_t i = 0; i < N; ++i) dT[i] = Cplx(dv[2 * i], dv[2 * i + 1]);
+    for (size_t s = 0; s < G; ++s)
+      for (size_t i = 0; i < N; ++i)
+        for (size_t j = 0; j < N; ++j) H[i][j] += part[s][i * N + j];
+  }
   std::vector<MPS> psiTrajectory() {
     std::vector<MPS> out;
     for (size_t t = 0; t < N; ++t)

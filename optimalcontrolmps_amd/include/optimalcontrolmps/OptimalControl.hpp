@@ -10,7 +10,8 @@
 //   void step(MPS&, double from, double to, bool forward = true) const;
 //   std::unique_ptr<Engine> makeEngine(const MPS& target, const MPS& init, size_t N) const;
 //   Engine: setShards(n), propagate(u, which), divT(), overlapFactor(),
-//           fidelities(), precomputeXiH(), hessianRows(u, F, divT, H), psiTrajectory().
+//           fidelities(), precomputeXiH(), hessianRows(u, F, divT, H),
+//           hessianFresh(u, F&, divT&, H) (all of the above for a new control), psiTrajectory().
 //
 // Host-side arithmetic kept verbatim from the reference: the regularisation
 // terms (:88-143), the gradient assembly g_i = dt Re(divT_i F i) (:240-246),
@@ -190,8 +191,12 @@ class OptimalControl {
   }
   rowmat calcHessian(const stdvec& u, const bool new_control) {
     if (new_control) {
-      calculatedXi = false;
-      calcPsiXiDivT(u);
+      // psi, xi, divT, xiHlist and the rows in one pipelined engine call
+      rowmat H = calcRegularizationHessian();
+      Cplx F;
+      engine->hessianFresh(u, F, divT, H);
+      calculatedXi = true;
+      return H;
     }
     if (!calculatedXi) {
       calcXi(u);

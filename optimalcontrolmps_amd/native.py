@@ -82,6 +82,7 @@ SIGNATURES = [
     ("ocg_div_t", C.c_int, [C.c_void_p, dp]),
     ("ocg_xi_dH", C.c_int, [C.c_void_p]),
     ("ocg_hessian_rows", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
+    ("ocg_hessian", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_kernel_stats", C.c_int, [C.c_void_p, C.c_int, dp, C.POINTER(C.c_long), dp, dp, C.POINTER(C.c_long)]),
     ("ocg_reset_stats", C.c_int, [C.c_void_p]),
@@ -247,6 +248,24 @@ class Engine:
         self._chk(lib().ocg_hessian_rows(self.h, pu, N, pr, len(r), Fa.ctypes.data_as(dp), dv.ctypes.data_as(dp),
                                          H.ctypes.data_as(dp)), "ocg_hessian_rows")
         return H
+
+    def hessian(self, u, rows=None, H=None):
+        """fused getHessian(u, new_control=true) fidelity part for `rows`
+        (default 1..N-2): returns (H, divT, F); device trajectories are left
+        as after propagate(u, 3) + xi_dH()"""
+        uu, pu = _d(u)
+        N = len(uu)
+        if rows is None:
+            rows = range(1, N - 1)
+        r, pr = _i(list(rows))
+        if H is None:
+            H = np.zeros((N, N))
+        H = np.ascontiguousarray(H, dtype=np.float64)
+        dv = np.zeros(2 * N)
+        Fa = np.zeros(2)
+        self._chk(lib().ocg_hessian(self.h, pu, N, pr, len(r), H.ctypes.data_as(dp), dv.ctypes.data_as(dp),
+                                    Fa.ctypes.data_as(dp)), "ocg_hessian")
+        return H, dv.view(np.complex128).copy(), complex(Fa[0], Fa[1])
 
     def state(self, which, t) -> MPS:
         fd, d, n = self._out()

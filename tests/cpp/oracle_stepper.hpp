@@ -82,6 +82,13 @@ class OracleTDMRG::Engine {
     for (size_t i = 0; i < N; ++i)
       for (size_t j = 0; j < N; ++j) H[i][j] += h[i * N + j];
   }
+  void hessianFresh(const stdvec& u, Cplx& F, std::vector<Cplx>& dT, rowmat& H) {
+    propagate(u, 3);
+    dT = divT();
+    F = overlapFactor();
+    precomputeXiH();
+    hessianRows(u, F, dT, H);
+  }
   std::vector<MPS> psiTrajectory() {
     std::vector<MPS> out;
     for (auto& m : oc.psi_t) out.push_back(from_oracle(m));

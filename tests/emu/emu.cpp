@@ -213,6 +213,53 @@ void emu_hessian(void* h, const int* dt_, const double* tgt, const int* di, cons
   });
 }
 
+// fused pipeline (ocg_hessian): k_pipeline then divT/F overlaps then k_row_overlaps
+void emu_hessian_fused(void* h, const int* dt_, const double* tgt, const int* di, const double* ini, const double* u,
+                       int N, double* H, double* divT, double* F) {
+  Emu& e = *static_cast<Emu*>(h);
+  e.slots(6 + 4 * N);
+  put(e, 1, dt_, tgt);
+  put(e, 0, di, ini);
+  OcgParams P = e.P;
+  const int psi = 6, xi = 6 + N, xih = 6 + 2 * N;
+  std::vector<int> rows, rb;
+  for (int i = 1; i + 1 < N; ++i) rows.push_back(i);
+  const int nrows = int(rows.size());
+  int total = 0;
+  for (int r = 0; r < nrows; ++r) { rb.push_back(total); total += N - 1 - rows[r]; }
+  rb.push_back(total);
+  std::vector<int> rsd(size_t(total) * P.nsq, 0);
+  std::vector<ocg::zc> rsx(size_t(total) * P.cap, ocg::c2(0, 0));
+  ocg::Pool rs{rsd.data(), rsx.data()};
+  std::vector<double> rn(nrows, 0.0);
+  std::vector<int> flags(2 * N, 0);
+  int err = 0;
+  launch(e, 2 + N + nrows, [&](char* smem) {
+    ocg::body_pipeline<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, xih, u, N, rows.data(),
+                           nrows, rb.data(), rs, rn.data(), flags.data(), 1, &err, e.stats);
+  });
+  std::vector<int> xs(N), ys(N);
+  std::vector<ocg::zc> pc(N + 1);
+  for (int i = 0; i < N; ++i) { xs[i] = xi + i; ys[i] = psi + i; }
+  launch(e, N, [&](char* smem) {
+    ocg::body_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), xs.data(), ys.data(), N, 1, pc.data(),
+                           e.stats + 3);
+  });
+  int a = psi + N - 1, b = 1;
+  launch(e, 1, [&](char* smem) {
+    ocg::body_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), &a, &b, 1, 0, pc.data() + N, e.stats + 3);
+  });
+  std::memset(H, 0, sizeof(double) * N * N);
+  launch(e, total, [&](char* smem) {
+    ocg::body_row_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), xih, rows.data(), nrows, rb.data(), rs,
+                               rn.data(), pc.data(), pc.data() + N, N, H, e.stats + 9);
+  });
+  for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
+  F[0] = pc[N].x;
+  F[1] = pc[N].y;
+  if (err) std::fprintf(stderr, "pipeline err %d\n", err);
+}
+
 }  // extern "C"
 
 extern "C" size_t emu_position(void* h, const int* dims, const double* x, int target, int back, int* od, double* ox) {

@@ -94,6 +94,11 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int, bool) {
   if (!((row_mask >> row) & 1) || s < 0) return old;
   return v;
 }
+#define __HIP_MEMORY_SCOPE_AGENT 0
+#define __hip_atomic_store(p, v, o, sc) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
+#define __hip_atomic_load(p, o, sc) __atomic_load_n((p), __ATOMIC_SEQ_CST)
+#define __builtin_amdgcn_s_sleep(x) ((void)0)
+inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 #define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
 #define __builtin_amdgcn_rcpf(x) emu_rcpf(x)
 #define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))

@@ -166,3 +166,36 @@ def test_cost_golden_via_gpu(states):
         assert abs(0.5 * (1 - abs(F) ** 2) - cost) < 5e-6
         f = eng.fidelities()
         assert np.abs(f[:-1] - np.array(fids[:-1])).max() < 1e-5
+
+
+@pytest.mark.parametrize("case", GOLDEN, ids=[c[0] for c in GOLDEN])
+def test_fused_hessian_vs_golden(states, oracle_golden, case):
+    """ocg_hessian (pipelined trajectories + rows, batched overlaps) against the fixtures"""
+    name, (L, p, N, J), Ui, Uf, dt, cut, maxm = case
+    u = oracle_golden[name + "/u"]
+    eng = engine(L, p, N, J, dt, cut, maxm)
+    eng.set_states(st_of(states, L, p, N, J, Uf), st_of(states, L, p, N, J, Ui))
+    H, divT, F = eng.hessian(u)
+    assert np.abs(divT - oracle_golden[name + "/divT"]).max() < 1e-9
+    assert abs(F - oracle_golden[name + "/F"][0]) < 1e-9
+    g = dt * (divT * F * 1j).real
+    assert np.abs(g - oracle_golden[name + "/grad"]).max() < 1e-6
+    Ho = oracle_golden[name + "/hess"]
+    assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+    # the device trajectories are left as after propagate(3) + xi_dH
+    assert list(eng.state(0, len(u) - 1).bond_dims()) == list(oracle_golden[name + "/psiT_dims"])
+
+
+def test_fused_equals_unfused_bitwise(states):
+    """same per-row arithmetic: the pipelined path reproduces the two-phase path exactly"""
+    L, p, N, J = 5, 5, 5, 1.0
+    u = np.random.default_rng(17).uniform(2, 10, 31)
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    eng.set_states(st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5))
+    divT, F, fid, H1 = run_engine_hessian(eng, u, st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5))
+    H2, divT2, F2 = eng.hessian(u)
+    assert np.array_equal(divT, divT2) and F == F2
+    assert np.array_equal(H1, H2)
+    rows = list(range(1, len(u) - 1))
+    parts = [eng.hessian(u, rows[k::4])[0] for k in range(4)]
+    assert np.array_equal(sum(parts), H2)
