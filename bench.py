@@ -7,11 +7,17 @@ L=5, Npart=5, d=4 (p=5), maxBondDim=80, cutoff 1e-8, J=1, tstep=0.01, T=2.0
 = ground states at U=2.5/50 (exact diagonalisation; synthetic controls).
 
 One "step" = one full getHessian(u, new_control=true)
-(src/OptimalControl.cpp:341-372): psi_t and xi_t trajectories, divT,
+(src/OptimalControl.cpp:341-372) per rank: psi_t and xi_t trajectories, divT,
 overlapFactor, xiHlist and all N_t-2 = 199 Hessian rows, plus the gradient
-assembly.  With --gpus N the rows are sharded zig-zag over the ranks (each
-rank recomputes the 400-step precompute) and the N_t x N_t partial Hessians
-are summed onto rank 0 with one RCCL reduce over xGMI.
+assembly.  Multi-GPU (one process per GPU):
+  --mode weak   (default) every rank evaluates the Hessian of its own control
+                vector (independent units, fixed work per GPU, no data-path
+                collective): value scales with N.
+  --mode strong one control vector; its rows are dealt zig-zag over the ranks
+                (each rank recomputes the 400-step precompute) and the N_t x N_t
+                partial Hessians are summed onto rank 0 with one RCCL reduce.
+                At config 1 one GPU already runs all 199 rows concurrently, so
+                the critical path (~200 steps) does not shrink with N.
 
 value = Hessian rows completed per second (whole job).
 """
@@ -39,6 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--mode", choices=["weak", "strong"], default="weak")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -61,8 +68,10 @@ def main():
     Nt = int(round(CFG["T"] / dt)) + 1
     ini = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, CFG["U_init"])[0], L, p, Q))
     tgt = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, CFG["U_target"])[0], L, p, Q))
-    u = np.random.default_rng(CFG["seed"]).uniform(2.0, 10.0, Nt)
-    rows = zigzag_rows(Nt - 2, rank, world)
+    strong = args.mode == "strong"
+    # weak: rank r evaluates its own control vector (seed + r); strong: one shared vector
+    u = np.random.default_rng(CFG["seed"] + (0 if strong else rank)).uniform(2.0, 10.0, Nt)
+    rows = zigzag_rows(Nt - 2, rank, world) if strong else list(range(1, Nt - 1))
 
     eng = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
     eng.set_states(tgt, ini)
@@ -74,7 +83,7 @@ def main():
         # and the batched <xiH_j|psiH> overlaps (ocg_hessian)
         H, divT, F = eng.hessian(u, rows)
         g = dt * (divT * F * 1j).real            # calcFidelityGrad (gamma = 0)
-        if world > 1:
+        if world > 1 and strong:
             Hdev.copy_(torch.from_numpy(H))
             dist.reduce(Hdev, dst=0)             # RCCL sum of disjoint row entries
         return g, H
@@ -98,13 +107,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    rows_total = (Nt - 2) * args.steps
+    rows_total = (Nt - 2) * args.steps * (1 if strong else world)
     value = rows_total / elapsed
     st_rows = eng.stats(5)       # k_pipeline: trajectories + row re-propagation (dominant)
     st_ovl = eng.stats(6)        # k_row_overlaps
     st_traj = eng.stats(0)
     row_steps = (Nt - 2) * (Nt - 3) // 2
-    sweep_steps = args.steps * (2 * (Nt - 1) * world + row_steps)
+    sweep_steps = args.steps * (2 * (Nt - 1) * world + row_steps * (1 if strong else world))
     result = None
     if rank == 0:
         launch_ms = st_rows["ms"] / max(1, st_rows["launches"])
@@ -120,13 +129,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.mode,
             "vs_baseline": None,
             "dtype": "c128/f64",
             "data": "synthetic GRAPE controls U(2,10) seed 20261015; ED ground states U=2.5 -> 50",
             "config": {"workload": "getHessian(u, new_control=true), config 1 (L=5 Npart=5 d=4 maxBondDim=80 "
                                    "tstep=0.01 T=2.0 GRAPE, N_t=201, 199 rows)",
-                       "rows_per_step": Nt - 2, "parallelism": f"rows sharded zig-zag over {world} GPU(s)"},
+                       "rows_per_step": (Nt - 2) * (1 if strong else world),
+                       "parallelism": (f"one control, rows sharded zig-zag over {world} GPU(s) + RCCL reduce" if strong
+                                       else f"{world} GPU(s), one full getHessian (own control vector) per GPU")},
             "sweep_steps_per_sec": sweep_steps / elapsed,
             "kernels": {
                 "pipeline": {"avg_ms": launch_ms, "launches": st_rows["launches"]},

@@ -136,6 +136,14 @@ __device__ __forceinline__ int udiv(int a, int b, int& r) {
 
 typedef int i4 __attribute__((vector_size(16)));
 
+// Circle-method pairing table for even block orders m <= kPairMaxM:
+// entry [pt_base(m) + r*m + x] = partner | (pair << 8) of index x in round
+// r < kPairMaxM - 1; rounds r >= m - 1 hold idle entries (x | 0xFF << 8).
+constexpr int kPairMaxM = 16;
+constexpr int kPairRounds = kPairMaxM - 1;
+constexpr int kPairTable = kPairRounds * 72;  // 15 * sum_{m = 2, 4, ..., 16} m
+__host__ __device__ constexpr int pt_base(int m) { return kPairRounds * (m - 2) * m / 4; }
+
 // ---------------------------------------------------------------- LDS map
 struct LdsLayout {
   // complex buffers (offsets in zc units)
@@ -146,7 +154,7 @@ struct LdsLayout {
   int ndbl;
   // int buffers (offsets in ints, after the double region)
   int DIMS, DIMX, MD, BOFF, BOFFT, TRO, TCO, THR, THC, THO, NQ, SIDE, GOFF, EOFF, MQ, POFF, KEPT, XOFF, YOFF, QST,
-      CDIM, COLD, COFF, EQ, RANK, JB, KIDX, ISCAL;
+      CDIM, COLD, COFF, EQ, RANK, JB, KIDX, PT, ISCAL;
   int nint;
   int bytes;
 };
@@ -208,6 +216,7 @@ __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   l.RANK = i; i = al(i + P.evcap);
   l.JB = i; i = al(i + P.evcap);
   l.KIDX = i; i = al(i + P.evcap);
+  l.PT = i; i = al(i + kPairTable);
   l.ISCAL = i; i += 16;
   l.nint = i;
   l.bytes = l.ncplx * 16 + l.ndbl * 8 + l.nint * 4;
@@ -230,7 +239,7 @@ struct Chain {
   lzp A, TH, G, G2, W, W2, X, Y, CR, S, GT, PH, ROT;
   LDS double *LAM, *PP, *SH, *RED, *SCAL, *PROF;
   LDS int *DIMS, *DIMX, *MD, *BOFF, *BOFFT, *TRO, *TCO, *THR, *THC, *THO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT,
-      *XOFF, *YOFF, *QST, *CDIM, *COLD, *COFF, *EQ, *RANK, *JB, *KIDX, *ISCAL;
+      *XOFF, *YOFF, *QST, *CDIM, *COLD, *COFF, *EQ, *RANK, *JB, *KIDX, *PT, *ISCAL;
   unsigned long long pf_last = 0;
   int pf_cur = 0;
   // algorithmic-traffic model accumulators (per lane, summed at the end)
@@ -249,7 +258,7 @@ struct Chain {
     TRO = ib + l.TRO; TCO = ib + l.TCO; THR = ib + l.THR; THC = ib + l.THC; THO = ib + l.THO; NQ = ib + l.NQ;
     SIDE = ib + l.SIDE; GOFF = ib + l.GOFF; EOFF = ib + l.EOFF; MQ = ib + l.MQ; POFF = ib + l.POFF;
     KEPT = ib + l.KEPT; XOFF = ib + l.XOFF; YOFF = ib + l.YOFF; QST = ib + l.QST; EQ = ib + l.EQ; RANK = ib + l.RANK;
-    JB = ib + l.JB; KIDX = ib + l.KIDX; CDIM = ib + l.CDIM; COLD = ib + l.COLD; COFF = ib + l.COFF;
+    JB = ib + l.JB; KIDX = ib + l.KIDX; PT = ib + l.PT; CDIM = ib + l.CDIM; COLD = ib + l.COLD; COFF = ib + l.COFF;
     ISCAL = ib + l.ISCAL;
   }
 
@@ -426,6 +435,16 @@ struct Chain {
   // directions out of every decomposition (guards the LDS capacities).
   __device__ OCG_INLINE void load_tables(const zc* gf, const zc* gb, const int* md) {
     for (int i = tid; i < 32; i += NT) PROF[i] = 0.0;
+    // circle-method pairing table (see jpair)
+    for (int e = tid; e < kPairTable; e += NT) {
+      int m = 2;
+      while (m < kPairMaxM && pt_base(m + 2) <= e) m += 2;
+      int x;
+      const int r = udiv(e - pt_base(m), m, x);
+      int px = x;
+      const int k = jpair(x, r, m, m, px);
+      PT[e] = k < 0 ? (x | (0xFF << 8)) : (px | (k << 8));
+    }
     for (int i = tid; i < P.gtotal; i += NT) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
     for (int i = tid; i < 2 * P.nsq; i += NT) MD[i] = md[i];
   }
@@ -578,18 +597,33 @@ struct Chain {
     if (x < px) { jd = c2(cs.x, 0); jo = cscale(cconj(e), -cs.y); }
     else { jd = cscale(cconj(e), cs.x); jo = c2(cs.y, 0); }
   }
-  // Gram element (i, j) of block q with the block data phase B needs
+  // Gram element (i, j) of block q, with what phase B needs in every round
   struct JD {
-    int i, j, n, m, go, po;  // n == 0: no element
+    int i, j, n, m, go, po, pti, ptj;  // n == 0: no element; pt*: pair-table row bases (-1: m > kPairMaxM)
   };
   __device__ __forceinline__ JD jd_of(int e, int nel) const {
-    JD r{0, 0, 0, 0, 0, 0};
+    JD r{0, 0, 0, 0, 0, 0, 0, 0};
     if (e < nel) {
       const int q = blk(GOFF, e);
       r.n = NQ[q]; r.m = MQ[q]; r.go = GOFF[q]; r.po = POFF[q];
       r.i = udiv(e - r.go, r.n, r.j);
+      if (r.m <= kPairMaxM) { r.pti = pt_base(r.m) + r.i; r.ptj = pt_base(r.m) + r.j; }
+      else { r.pti = -1; r.ptj = -1; }
     }
     return r;
+  }
+  // partner / pair of index x (table row base ptx) in round rnd; -1 if idle
+  __device__ __forceinline__ int jlook(int x, int ptx, int rnd, int m, int n, int& px) const {
+    if (rnd >= m - 1) { px = x; return -1; }
+    int k;
+    if (ptx >= 0) {
+      const int v = PT[ptx + rnd * m];
+      px = v & 255;
+      k = v >> 8;
+    } else {
+      k = jpair(x, rnd, m, n, px);
+    }
+    return (px < n) ? k : -1;
   }
   // rotation pair t = (block q, pair k)
   struct JP {
@@ -603,6 +637,15 @@ struct Chain {
     }
     return r;
   }
+  // rotate (p, q) iff |g_pq|^2 > tol^2 |g_pp g_qq| + (1e-18 (|g_pp| + |g_qq|))^2 (tol = 1e-14):
+  // the Demmel-Veselic test bounds the orthonormality defect of the derived
+  // factor, g_pq / (sigma_p sigma_q), by tol; the second term stops rotations
+  // that are below working precision of the diagonal.  The same predicate is
+  // the convergence test, so a converged sweep performs no rotation.
+  __device__ __forceinline__ static bool jneed(double b2, double app, double aqq) {
+    const double s = fabs(app) + fabs(aqq);
+    return b2 > 1e-28 * fabs(app * aqq) + 1e-36 * s * s && b2 > 0.0;
+  }
   // Phase A: complex Jacobi rotation zeroing g[p][q] of pair t in round rnd.
   // With D = aqq - app, b = g[p][q], r = |b| (the classical tan formula
   // t = sgn(D) / (|tau| + sqrt(1 + tau^2)), tau = D / (2 r), cleared of divisions):
@@ -614,35 +657,32 @@ struct Chain {
     zc cs = c2(1.0, 0.0), e = c2(1.0, 0.0);
     double shift = 0.0;
     if (rnd < M) {
-      int a, b;
-      if (d.k == 0) { a = rnd; b = M; }
-      else {
-        a = rnd + d.k; if (a >= M) a -= M;
-        b = rnd - d.k; if (b < 0) b += M;
-      }
+      int a = rnd + d.k, b = rnd - d.k;
+      if (d.k == 0) b = M;
+      if (a >= M) a -= M;
+      if (b < 0) b += M;
       const int pp_ = a < b ? a : b, qq_ = a < b ? b : a;
       if (qq_ < n) {
         lzp g = Gc + d.go;
         zc bv = g[pp_ * n + qq_];
         double app = zc(g[pp_ * n + pp_]).x, aqq = zc(g[qq_ * n + qq_]).x;
-        const double sz = fabs(app) + fabs(aqq);
-        const double mb = fmax(fabs(bv.x), fabs(bv.y));
-        // skip rotations whose off-diagonal is below working precision of the diagonal
-        if (mb > 1e-300 && mb > 1e-18 * sz) {
+        double r2 = bv.x * bv.x + bv.y * bv.y;
+        if (jneed(r2, app, aqq)) {
           // power-of-two rescale keeps r^2 and D^2 in range (exact, rare)
           double sc = 1.0;
+          const double mb = fmax(fabs(bv.x), fabs(bv.y)), sz = fabs(app) + fabs(aqq);
           if (mb < 1e-120 || mb > 1e120 || sz > 1e120) {
             sc = ldexp(1.0, -ilogb(fmax(mb, sz)));
             bv = cscale(bv, sc); app *= sc; aqq *= sc;
+            r2 = bv.x * bv.x + bv.y * bv.y;
           }
-          const double r2 = bv.x * bv.x + bv.y * bv.y;
           const double rinv = rsqrt(r2), r = r2 * rinv;
           const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
           const double E = fabs(D) + sqrt(fma(D, D, 4.0 * r2));
           const double h = rsqrt(fma(E, E, 4.0 * r2));
           cs = c2(E * h, sg * 2.0 * r * h);
           e = c2(bv.x * rinv, bv.y * rinv);
-          shift = sg * 2.0 * r2 / E / sc;
+          shift = sg * 2.0 * r2 / (E * sc);
         }
       }
     }
@@ -650,25 +690,33 @@ struct Chain {
     ROT[2 * t + 1] = e;
     SH[t] = shift;
   }
+  // coefficients of column x of J for pair (cs = (c, s), e), branch-free:
+  //   x = p (x < partner): J[p][p] = c,     J[q][p] = -s e*
+  //   x = q:               J[q][q] = c e*,  J[p][q] = s
+  __device__ __forceinline__ static void jcol(bool isp, zc cs, zc e, zc& jd, zc& jo) {
+    const zc ce = cscale(cconj(e), cs.x), se = cscale(cconj(e), -cs.y);
+    jd = isp ? c2(cs.x, 0.0) : ce;
+    jo = isp ? se : c2(cs.y, 0.0);
+  }
   // Phase B: G'[i][j] = (J^H G J)[i][j] and W'[i][j] = (W J)[i][j]
   __device__ __forceinline__ void jupd(const JD& d, int rnd, lzp Gc, lzp Wc, lzp Gn, lzp Wn, bool lastr, int fl) {
     if (d.n == 0) return;
     const int i = d.i, j = d.j, n = d.n, m = d.m, loc = i * n + j;
     lzp gs = Gc + d.go, ws = Wc + d.go;
-    int pj = j, pi = i;
-    const int kj = (m > 0) ? jpair(j, rnd, m, n, pj) : -1;
-    const int ki = (m > 0) ? jpair(i, rnd, m, n, pi) : -1;
+    int pj, pi;
+    const int kj = jlook(j, d.ptj, rnd, m, n, pj);
+    const int ki = jlook(i, d.pti, rnd, m, n, pi);
     zc jjj = c2(1, 0), jpj = c2(0, 0), jii = c2(1, 0), jpi = c2(0, 0);
     bool rotj = false, roti = false;
     if (kj >= 0) {
       const zc cs = ROT[2 * (d.po + kj)], ee = ROT[2 * (d.po + kj) + 1];
       rotj = cs.y != 0.0;
-      jcol(j, pj, cs, ee, jjj, jpj);
+      jcol(j < pj, cs, ee, jjj, jpj);
     }
     if (ki >= 0) {
       const zc cs = ROT[2 * (d.po + ki)], ee = ROT[2 * (d.po + ki) + 1];
       roti = cs.y != 0.0;
-      jcol(i, pi, cs, ee, jii, jpi);
+      jcol(i < pi, cs, ee, jii, jpi);
     }
     // W'[i][j] = W[i][j] J[j][j] + W[i][j'] J[j'][j]
     zc w = cmul(ws[loc], jjj);
@@ -691,12 +739,60 @@ struct Chain {
         cjacc(out, jpi, r1);
       }
     }
-    // convergence: an off-diagonal entry above 1e-15 of its diagonal pair
-    if (lastr && i < j) {
-      const double sz = fabs(zc(gs[i * n + i]).x) + fabs(zc(gs[j * n + j]).x);
-      if (cabs2(out) > 1e-30 * sz * sz) atomicOr((int*)&ISCAL[fl], 1);
-    }
+    // convergence: the rotation predicate on the output of the sweep's last round
+    if (lastr && i < j && jneed(cabs2(out), zc(gs[i * n + i]).x, zc(gs[j * n + j]).x))
+      ISCAL[fl] = 1;  // benign race: every writer stores 1
     Gn[d.go + loc] = out;
+  }
+  // Branch-free phase B for blocks of order m <= kPairMaxM (all blocks of the
+  // decomposition): the pairing comes from the table, idle / padded /
+  // unrotated indices get identity coefficients by selects, and every element
+  // computes both its G' and W' entries.
+  __device__ __forceinline__ void jupd_fast(const JD& d, bool valid, int rnd, lzp Gc, lzp Wc, lzp Gn, lzp Wn,
+                                            bool lastr, int fl) {
+    const int i = d.i, j = d.j, n = d.n > 0 ? d.n : 1, loc = i * n + j;
+    lzp gs = Gc + d.go, ws = Wc + d.go;
+    const int vj = PT[d.ptj + rnd * d.m], vi = PT[d.pti + rnd * d.m];
+    int pj = vj & 255, kj = vj >> 8, pi = vi & 255, ki = vi >> 8;
+    const bool aj = kj != 0xFF && pj < n, ai = ki != 0xFF && pi < n;
+    pj = aj ? pj : j;
+    pi = ai ? pi : i;
+    kj = aj ? kj : 0;
+    ki = ai ? ki : 0;
+    const zc csj = ROT[2 * (d.po + kj)], ej = ROT[2 * (d.po + kj) + 1];
+    const zc csi = ROT[2 * (d.po + ki)], ei = ROT[2 * (d.po + ki) + 1];
+    const double sh = SH[d.po + kj];
+    const zc g00 = gs[loc], g01 = gs[i * n + pj], g10 = gs[pi * n + j], g11 = gs[pi * n + pj];
+    const zc w0 = ws[loc], w1 = ws[i * n + pj];
+    const bool rotj = aj && csj.y != 0.0, roti = ai && csi.y != 0.0;
+    zc jjj, jpj, jii, jpi;
+    jcol(j < pj, csj, ej, jjj, jpj);
+    jcol(i < pi, csi, ei, jii, jpi);
+    jjj = rotj ? jjj : c2(1, 0);
+    jpj = rotj ? jpj : c2(0, 0);
+    jii = roti ? jii : c2(1, 0);
+    jpi = roti ? jpi : c2(0, 0);
+    // W'[i][j] = W[i][j] J[j][j] + W[i][j'] J[j'][j]
+    zc w = cmul(w0, jjj);
+    cacc(w, w1, jpj);
+    // G'[i][j] = sum_{k in {i,i'}} sum_{l in {j,j'}} conj(J[k][i]) G[k][l] J[l][j]
+    zc r0 = cmul(g00, jjj);
+    cacc(r0, g01, jpj);
+    zc r1 = cmul(g10, jjj);
+    cacc(r1, g11, jpj);
+    zc out = cjmul(jii, r0);
+    cjacc(out, jpi, r1);
+    // the rotated 2x2 block: exact zero off-diagonal, shifted diagonal
+    const bool zero = rotj && roti && pi == j;
+    const bool diag = rotj && i == j;
+    out = zero ? c2(0, 0) : out;
+    out = diag ? c2(g00.x + (j < pj ? -sh : sh), 0) : out;
+    if (valid) {
+      Wn[d.go + loc] = w;
+      Gn[d.go + loc] = out;
+      if (lastr && i < j && jneed(cabs2(out), zc(gs[i * n + i]).x, zc(gs[j * n + j]).x))
+        ISCAL[fl] = 1;  // benign race: every writer stores 1
+    }
   }
   // Parallel (round-robin) complex Jacobi on all Gram blocks at once.
   // Block q: n = NQ[q] at G + GOFF[q]; eigenvectors accumulated in W.
@@ -714,6 +810,8 @@ struct Chain {
     const int nel = GOFF[P.Q1];
     JD dB[JB_IT];
     JP dA[JA_IT];
+    // every block small enough for the pairing table and all elements cached
+    const bool fast = maxr <= kPairRounds && nel <= JB_IT * NT;
 #pragma unroll
     for (int it = 0; it < JB_IT; ++it) dB[it] = jd_of(it * NT + tid, nel);
 #pragma unroll
@@ -725,13 +823,20 @@ struct Chain {
         if (rnd == 0 && tid == 0) ISCAL[I_FLAG + (sweep + 1) % 3] = 0;
         pf(13);
 #pragma unroll
-        for (int it = 0; it < JA_IT; ++it) jrot(dA[it], it * NT + tid, rnd, Gc);
+        for (int it = 0; it < JA_IT; ++it)
+          if (it * NT < npair) jrot(dA[it], it * NT + tid, rnd, Gc);
         for (int t = JA_IT * NT + tid; t < npair; t += NT) jrot(jp_of(t, npair), t, rnd, Gc);
         sync();
         pf(14);
         const bool lastr = rnd == maxr - 1;
+        if (fast) {
 #pragma unroll
-        for (int it = 0; it < JB_IT; ++it) jupd(dB[it], rnd, Gc, Wc, Gn, Wn, lastr, fl);
+          for (int it = 0; it < JB_IT; ++it)
+            if (it * NT < nel) jupd_fast(dB[it], it * NT + tid < nel, rnd, Gc, Wc, Gn, Wn, lastr, fl);
+        } else {
+#pragma unroll
+          for (int it = 0; it < JB_IT; ++it) jupd(dB[it], rnd, Gc, Wc, Gn, Wn, lastr, fl);
+        }
         for (int e = JB_IT * NT + tid; e < nel; e += NT) jupd(jd_of(e, nel), rnd, Gc, Wc, Gn, Wn, lastr, fl);
         sync();
         pf(3);
@@ -875,7 +980,7 @@ struct Chain {
       for (int e = tid; e < T; e += NT) {
         const int q = EQ[e], jb = JB[e];
         if (RANK[e] < m && jb < bound[q]) {
-          atomicAdd((int*)&KEPT[q], 1);
+          __hip_atomic_fetch_add(&KEPT[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_add_u32
           KIDX[EOFF[q] + jb] = e - EOFF[q];
           kw += LAM[e];
         }

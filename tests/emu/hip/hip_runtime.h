@@ -75,6 +75,8 @@ inline unsigned long long __ballot(int pred) {
   return m;
 }
 inline int __popcll(unsigned long long m) { return __builtin_popcountll(m); }
+inline double emu_rcp(double x) { return 1.0 / x; }
+#define __builtin_amdgcn_rcp(x) emu_rcp(x)
 inline double rsqrt(double x) { return 1.0 / std::sqrt(x); }
 inline int max(int a, int b) { return a > b ? a : b; }
 inline int min(int a, int b) { return a < b ? a : b; }
@@ -95,6 +97,8 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int, bool) {
   return v;
 }
 #define __HIP_MEMORY_SCOPE_AGENT 0
+#define __HIP_MEMORY_SCOPE_WORKGROUP 0
+#define __hip_atomic_fetch_add(p, v, o, sc) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
 #define __hip_atomic_store(p, v, o, sc) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
 #define __hip_atomic_load(p, o, sc) __atomic_load_n((p), __ATOMIC_SEQ_CST)
 #define __builtin_amdgcn_s_sleep(x) ((void)0)

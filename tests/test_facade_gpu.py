@@ -7,6 +7,12 @@ import numpy as np
 import pytest
 
 import facade_build as fb
+
+# absolute floor of the central-difference gradient (eps = 1e-5): the cost
+# carries ~1e-13 jitter from truncation decisions (cutoff 1e-8), i.e. ~1e-8 in
+# (J+ - J-)/2eps; the reference's purely relative check is flaky on entries
+# that small (it seeds with srand(time), tests/GradientTests.cpp:43)
+FD_FLOOR = 5e-8
 import reference_goldens as RG
 
 pytestmark = pytest.mark.gpu
@@ -44,7 +50,7 @@ def test_gpu_facade_gradient_fd(statedir):
     for mode in ("", "_bfgs"):
         for alg, rel in [("grape", 1e-3), ("group", 2e-3)]:
             a, n = A(r[f"{alg}_ana{mode}"]), A(r[f"{alg}_num{mode}"])
-            assert np.all(np.abs(a - n)[1:-1] <= np.abs(n[1:-1]) * rel + 1e-12)
+            assert np.all(np.abs(a - n)[1:-1] <= np.abs(n[1:-1]) * rel + FD_FLOOR)
     assert np.abs(A(r["grad_seq"]) - A(r["grad_par"]))[1:-1].max() <= 1e-11
 
 
