@@ -26,7 +26,7 @@ using ocg::zc;
 static inline zc mkz(double x, double y) { zc r; r.x = x; r.y = y; return r; }
 
 #ifndef OCG_NT
-#define OCG_NT 64
+#define OCG_NT 128
 #endif
 static constexpr int NT = OCG_NT;
 
