@@ -263,10 +263,16 @@ struct Chain {
   }
 
   __device__ __forceinline__ void sync() { __syncthreads(); }
+  // LDS visibility among the lanes of one wave (no block barrier)
+  __device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   // Diagnostic build only (-DOCG_PROFILE): thread 0 charges the shader-clock
   // cycles since the previous stamp to the category that was running.
   // Categories: 0 build_theta 1 apply_gate 2 gram 3 jacobi 4 rank/truncate
-  // 5 factors X/Y 6 scatter 7 gauge write-back 8 overlap 9 phases/norms
+  // 5 factors X/Y (incl. the two-site write) 6 (unused) 7 gauge write-back 8 overlap 9 phases/norms
   // 10 load/store 11 apply_dH zip 12 other.
   __device__ __forceinline__ void pf(int cat) {
 #ifdef OCG_PROFILE
@@ -858,9 +864,13 @@ struct Chain {
   // The Gram matrix is formed on the smaller side of each block; the factor
   // on the other side is derived from TH.
   // If `normalize`, the norm-carrying factor is divided by sqrt(kept weight).
+  // ts > 0: two-site update of sites (ts, ts+1): the new bond ts is written
+  // to DIMS and X / Y go straight into the site tensors (rows (n1, a) of
+  // site ts, cols (n2, c) of site ts+1) instead of the X / Y scratch.
   // `bound` = per-sector rank bound of the new bond (MD row, or MDZ row in
   // the dH zip-up); vectors beyond it are numerically zero and dropped.
-  __device__ OCG_INLINE void decompose(int dir, double cutoff, int maxm, bool normalize, const LDS int* bound) {
+  __device__ OCG_INLINE void decompose(int dir, double cutoff, int maxm, bool normalize, const LDS int* bound,
+                                       int ts = 0) {
     pf(16);
     const int Q1 = P.Q1;
     if (w0) {
@@ -913,90 +923,170 @@ struct Chain {
     pf(4);
     // eigenvalues (clamped at 0) and their blocks
     const int T = EOFF[Q1];
-    {
-      for (int base = 0; base < T; base += NT) {
-        const int e = base + tid;
+    if (T <= 64) {
+      // one wave: ranking, truncation and the kept set in registers, ballot
+      // counts per sector, wave-level fences instead of block barriers
+      if (w0) {
+        const int e = lane;
+        const bool act = e < T;
         const int q = blk(EOFF, e);
-        if (e < T) {
+        double lam = 0.0;
+        if (act) {
           const int i = e - EOFF[q], n = NQ[q];
-          const double lam = zc(Gc[GOFF[q] + i * n + i]).x;
-          LAM[e] = lam > 0 ? lam : 0.0;
+          const double g = zc(Gc[GOFF[q] + i * n + i]).x;
+          lam = g > 0 ? g : 0.0;
+          LAM[e] = lam;
           EQ[e] = q;
         }
-      }
-    }
-    sync();
-    // global rank (descending; ties by flat index) and rank within the block
-    // (the competitors are read as LDS broadcasts, four in flight)
-    for (int e = tid; e < T; e += NT) {
-      const double le = LAM[e];
-      const int be = EQ[e];
-      int rk = 0, jb = 0;
-      int f = 0;
-      for (; f + 3 < T; f += 4) {
-        const double l0 = LAM[f], l1 = LAM[f + 1], l2 = LAM[f + 2], l3 = LAM[f + 3];
-        const int b0 = EQ[f], b1 = EQ[f + 1], b2 = EQ[f + 2], b3 = EQ[f + 3];
-        const int c0 = (l0 > le) || (l0 == le && f < e), c1 = (l1 > le) || (l1 == le && f + 1 < e);
-        const int c2_ = (l2 > le) || (l2 == le && f + 2 < e), c3 = (l3 > le) || (l3 == le && f + 3 < e);
-        rk += c0 + c1 + c2_ + c3;
-        jb += (c0 & (b0 == be)) + (c1 & (b1 == be)) + (c2_ & (b2 == be)) + (c3 & (b3 == be));
-      }
-      for (; f < T; ++f) {
-        const double lf = LAM[f];
-        const int c = (lf > le) || (lf == le && f < e);
-        rk += c;
-        jb += c & (EQ[f] == be);
-      }
-      RANK[e] = rk;
-      JB[e] = jb;
-      PP[rk] = le;
-    }
-    sync();
-    // truncation (ITensor truncate; relative cutoff; floor 1e-30): the
-    // discarded set {j >= 1 : j >= maxm or sum_{i>=j} PP[i] < cutoff*total or
-    // PP[j] <= 1e-30 total} is a suffix of the sorted spectrum
-    if (w0) {
-      double total = 0;
-      for (int b = 0; b < T; b += 64) total += wsum((b + lane < T) ? PP[b + lane] : 0.0);
-      const double cut = cutoff * total, floor_ = 1e-30 * total;
-      double carry = 0;
-      int nd = 0;
-      for (int cb = 0; cb < T; cb += 64) {
-        const int j = T - 1 - cb - lane;  // lane 0 = smallest
+        wsync();
+        // global rank (descending; ties by flat index) and rank within the block
+        int rk = 0, jb = 0;
+        if (act) {
+          int f = 0;
+          for (; f + 3 < T; f += 4) {
+            const double l0 = LAM[f], l1 = LAM[f + 1], l2 = LAM[f + 2], l3 = LAM[f + 3];
+            const int b0 = EQ[f], b1 = EQ[f + 1], b2 = EQ[f + 2], b3 = EQ[f + 3];
+            const int c0 = (l0 > lam) || (l0 == lam && f < e), c1 = (l1 > lam) || (l1 == lam && f + 1 < e);
+            const int c2_ = (l2 > lam) || (l2 == lam && f + 2 < e), c3 = (l3 > lam) || (l3 == lam && f + 3 < e);
+            rk += c0 + c1 + c2_ + c3;
+            jb += (c0 & (b0 == q)) + (c1 & (b1 == q)) + (c2_ & (b2 == q)) + (c3 & (b3 == q));
+          }
+          for (; f < T; ++f) {
+            const double lf = LAM[f];
+            const int c = (lf > lam) || (lf == lam && f < e);
+            rk += c;
+            jb += c & (EQ[f] == q);
+          }
+          PP[rk] = lam;
+        }
+        wsync();
+        // truncation (ITensor truncate; relative cutoff; floor 1e-30): the
+        // discarded set {j >= 1 : j >= maxm or sum_{i>=j} PP[i] < cutoff*total
+        // or PP[j] <= 1e-30 total} is a suffix of the sorted spectrum
+        const double total = wsum(act ? PP[lane] : 0.0);
+        const double cut = cutoff * total, floor_ = 1e-30 * total;
+        const int j = T - 1 - lane;  // lane 0 = smallest
         const double v = j >= 0 ? PP[j] : 0.0;
-        const double inc = wscan(v);
-        const double suf = carry + inc;
+        const double suf = wscan(v);
         const bool disc = j >= 1 && (j >= maxm || suf < cut || v <= floor_);
-        nd += __popcll(__ballot(disc));
-        carry += rdlane(inc, 63);
-      }
-      if (lane == 0) { ISCAL[I_M] = T - nd; SCAL[S_TOTAL] = total; }
-    }
-    sync();
-    // kept vectors: global rank < m and within the sector's rank bound
-    {
-      const int m = ISCAL[I_M];
-      double kw = 0;
-      for (int e = tid; e < T; e += NT) {
-        const int q = EQ[e], jb = JB[e];
-        if (RANK[e] < m && jb < bound[q]) {
-          __hip_atomic_fetch_add(&KEPT[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_add_u32
-          KIDX[EOFF[q] + jb] = e - EOFF[q];
-          kw += LAM[e];
+        const int m = T - __popcll(__ballot(disc));
+        // kept vectors: global rank < m and within the sector's rank bound
+        const bool kept = act && rk < m && jb < bound[q];
+        if (kept) KIDX[EOFF[q] + jb] = e - EOFF[q];
+        const double kw = wsum(kept ? lam : 0.0);
+        int kq = 0;
+        for (int s = 0; s < Q1; ++s) {
+          const int c = __popcll(__ballot(kept && q == s));
+          kq = (lane == s) ? c : kq;
+        }
+        const int R = lane < Q1 ? THR[lane] : 0, C = lane < Q1 ? THC[lane] : 0;
+        const int ix = wscan(R * kq), iy = wscan(kq * C);
+        if (lane < Q1) { KEPT[lane] = kq; XOFF[lane] = ix - R * kq; YOFF[lane] = iy - kq * C; }
+        if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; ISCAL[I_M] = m; SCAL[S_TOTAL] = total; SCAL[S_KEPTW] = kw; }
+        if (ts) {  // two-site update: new bond ts and the layouts of sites ts, ts+1
+          if (lane < Q1) DIMS[ts * Q1 + lane] = kq;
+          wsync();
+          site_offsets(ts);
+          site_offsets(ts + 1);
         }
       }
-      kw = block_sum(kw);
-      if (tid == 0) SCAL[S_KEPTW] = kw;
+      sync();
+    } else {
+      {
+        for (int base = 0; base < T; base += NT) {
+          const int e = base + tid;
+          const int q = blk(EOFF, e);
+          if (e < T) {
+            const int i = e - EOFF[q], n = NQ[q];
+            const double lam = zc(Gc[GOFF[q] + i * n + i]).x;
+            LAM[e] = lam > 0 ? lam : 0.0;
+            EQ[e] = q;
+          }
+        }
+      }
+      sync();
+      // global rank (descending; ties by flat index) and rank within the block
+      // (the competitors are read as LDS broadcasts, four in flight)
+      for (int e = tid; e < T; e += NT) {
+        const double le = LAM[e];
+        const int be = EQ[e];
+        int rk = 0, jb = 0;
+        int f = 0;
+        for (; f + 3 < T; f += 4) {
+          const double l0 = LAM[f], l1 = LAM[f + 1], l2 = LAM[f + 2], l3 = LAM[f + 3];
+          const int b0 = EQ[f], b1 = EQ[f + 1], b2 = EQ[f + 2], b3 = EQ[f + 3];
+          const int c0 = (l0 > le) || (l0 == le && f < e), c1 = (l1 > le) || (l1 == le && f + 1 < e);
+          const int c2_ = (l2 > le) || (l2 == le && f + 2 < e), c3 = (l3 > le) || (l3 == le && f + 3 < e);
+          rk += c0 + c1 + c2_ + c3;
+          jb += (c0 & (b0 == be)) + (c1 & (b1 == be)) + (c2_ & (b2 == be)) + (c3 & (b3 == be));
+        }
+        for (; f < T; ++f) {
+          const double lf = LAM[f];
+          const int c = (lf > le) || (lf == le && f < e);
+          rk += c;
+          jb += c & (EQ[f] == be);
+        }
+        RANK[e] = rk;
+        JB[e] = jb;
+        PP[rk] = le;
+      }
+      sync();
+      // truncation (ITensor truncate; relative cutoff; floor 1e-30): the
+      // discarded set {j >= 1 : j >= maxm or sum_{i>=j} PP[i] < cutoff*total or
+      // PP[j] <= 1e-30 total} is a suffix of the sorted spectrum
+      if (w0) {
+        double total = 0;
+        for (int b = 0; b < T; b += 64) total += wsum((b + lane < T) ? PP[b + lane] : 0.0);
+        const double cut = cutoff * total, floor_ = 1e-30 * total;
+        double carry = 0;
+        int nd = 0;
+        for (int cb = 0; cb < T; cb += 64) {
+          const int j = T - 1 - cb - lane;  // lane 0 = smallest
+          const double v = j >= 0 ? PP[j] : 0.0;
+          const double inc = wscan(v);
+          const double suf = carry + inc;
+          const bool disc = j >= 1 && (j >= maxm || suf < cut || v <= floor_);
+          nd += __popcll(__ballot(disc));
+          carry += rdlane(inc, 63);
+        }
+        if (lane == 0) { ISCAL[I_M] = T - nd; SCAL[S_TOTAL] = total; }
+      }
+      sync();
+      // kept vectors: global rank < m and within the sector's rank bound
+      {
+        const int m = ISCAL[I_M];
+        double kw = 0;
+        for (int e = tid; e < T; e += NT) {
+          const int q = EQ[e], jb = JB[e];
+          if (RANK[e] < m && jb < bound[q]) {
+            __hip_atomic_fetch_add(&KEPT[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // ds_add_u32
+            KIDX[EOFF[q] + jb] = e - EOFF[q];
+            kw += LAM[e];
+          }
+        }
+        kw = block_sum(kw);
+        if (tid == 0) SCAL[S_KEPTW] = kw;
+      }
+      sync();
+      if (w0) {
+        const int q = lane;
+        const int k = q < Q1 ? KEPT[q] : 0, R = q < Q1 ? THR[q] : 0, C = q < Q1 ? THC[q] : 0;
+        const int ix = wscan(R * k), iy = wscan(k * C);
+        if (q < Q1) { XOFF[q] = ix - R * k; YOFF[q] = iy - k * C; }
+        if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; }
+      }
+      sync();
+      if (ts) {
+        if (w0 && lane < Q1) DIMS[ts * Q1 + lane] = KEPT[lane];
+        sync();
+        if (NW == 1) {
+          site_offsets(ts);
+          site_offsets(ts + 1);
+        } else if (tid < 64) site_offsets(ts);
+        else if (tid < 128) site_offsets(ts + 1);
+        sync();
+      }
     }
-    sync();
-    if (w0) {
-      const int q = lane;
-      const int k = q < Q1 ? KEPT[q] : 0, R = q < Q1 ? THR[q] : 0, C = q < Q1 ? THC[q] : 0;
-      const int ix = wscan(R * k), iy = wscan(k * C);
-      if (q < Q1) { XOFF[q] = ix - R * k; YOFF[q] = iy - k * C; }
-      if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; }
-    }
-    sync();
     pf(5);
     // materialise X (R x k) and Y (k x C) per block
     const double kwv = SCAL[S_KEPTW];
@@ -1023,7 +1113,11 @@ struct Chain {
           if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
-        X[e] = out;
+        if (ts) {  // rows (n1, a) of site ts
+          int o;
+          const int n1 = seg_in(TRO, q, row, o);
+          site(ts)[bo(ts, q - n1, n1) + (row - o) * k + j] = out;
+        } else X[e] = out;
       }
     }
     for (int base = 0; base < yt; base += NT) {
@@ -1047,45 +1141,11 @@ struct Chain {
           if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
-        Y[e] = out;
-      }
-    }
-    sync();
-  }
-
-  // write X (rows (n1,a)) into site i1 and Y (cols (n2,c)) into site i1+1
-  __device__ OCG_INLINE void scatter_two_site(int i1) {
-    pf(6);
-    const int r = i1 + 1;
-    if (w0 && lane < P.Q1) DIMS[i1 * P.Q1 + lane] = KEPT[lane];
-    sync();
-    if (NW == 1) {
-      site_offsets(i1);
-      site_offsets(r);
-    } else if (tid < 64) site_offsets(i1);
-    else if (tid < 128) site_offsets(r);
-    sync();
-    const int xt = XOFF[P.Q1], yt = YOFF[P.Q1];
-    for (int base = 0; base < xt; base += NT) {
-      const int e = base + tid;
-      const int q = blk(XOFF, e);
-      if (e < xt) {
-        const int k = KEPT[q];
-        int j, o;
-        const int row = udiv(e - XOFF[q], k, j);
-        const int n1 = seg_in(TRO, q, row, o);
-        site(i1)[bo(i1, q - n1, n1) + (row - o) * k + j] = X[e];
-      }
-    }
-    for (int base = 0; base < yt; base += NT) {
-      const int e = base + tid;
-      const int q = blk(YOFF, e);
-      if (e < yt) {
-        const int C = THC[q];
-        int col, o;
-        const int j = udiv(e - YOFF[q], C, col);
-        const int n2 = seg_in(TCO, q, col, o);
-        site(r)[bo(r, q, n2) + j * d(r, q + n2) + (col - o)] = Y[e];
+        if (ts) {  // cols (n2, c) of site ts+1
+          int o;
+          const int n2 = seg_in(TCO, q, col, o);
+          site(ts + 1)[bo(ts + 1, q, n2) + j * d(ts + 1, q + n2) + (col - o)] = out;
+        } else Y[e] = out;
       }
     }
     sync();
@@ -1267,8 +1327,7 @@ struct Chain {
       const bool more = g + 1 < P.ngates;
       const int ni1 = more ? P.gate_i1[g + 1] : 0, ni2 = ni1 + 1;
       const int dir = (more && ni1 >= i2) ? kFromleft : kFromright;
-      decompose(dir, P.cutoff, P.maxm, true, MD + i1 * P.Q1);
-      scatter_two_site(i1);
+      decompose(dir, P.cutoff, P.maxm, true, MD + i1 * P.Q1, i1);  // writes sites i1, i2
       centre = (dir == kFromleft) ? i2 : i1;
       const int target = !more ? 1 : (dir == kFromleft ? ni1 : ni2);
       position(centre, target);

@@ -106,3 +106,5 @@ inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 #define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
 #define __builtin_amdgcn_rcpf(x) emu_rcpf(x)
 #define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))
+#define __builtin_amdgcn_fence(o, s) __atomic_thread_fence(__ATOMIC_SEQ_CST)
+#define __builtin_amdgcn_wave_barrier() emu_wbar->arrive_and_wait()
