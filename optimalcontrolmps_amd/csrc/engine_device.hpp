@@ -657,6 +657,62 @@ struct Chain {
   // t = sgn(D) / (|tau| + sqrt(1 + tau^2)), tau = D / (2 r), cleared of divisions):
   //   R = sqrt(D^2 + 4 r^2), E = |D| + R, c = E / sqrt(E^2 + 4 r^2),
   //   s = sgn(D) 2 r / sqrt(E^2 + 4 r^2), shift = sgn(D) 2 r^2 / E, e = b / r.
+  __device__ __forceinline__ static void jrot_val(zc bv, double app, double aqq, zc& cs, zc& e, double& shift) {
+    cs = c2(1.0, 0.0);
+    e = c2(1.0, 0.0);
+    shift = 0.0;
+    double r2 = bv.x * bv.x + bv.y * bv.y;
+    if (jneed(r2, app, aqq)) {
+      // power-of-two rescale keeps r^2 and D^2 in range (exact, rare)
+      double sc = 1.0;
+      const double mb = fmax(fabs(bv.x), fabs(bv.y)), sz = fabs(app) + fabs(aqq);
+      if (mb < 1e-120 || mb > 1e120 || sz > 1e120) {
+        sc = ldexp(1.0, -ilogb(fmax(mb, sz)));
+        bv = cscale(bv, sc); app *= sc; aqq *= sc;
+        r2 = bv.x * bv.x + bv.y * bv.y;
+      }
+      const double rinv = rsqrt(r2), r = r2 * rinv;
+      const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
+      const double E = fabs(D) + sqrt(fma(D, D, 4.0 * r2));
+      const double h = rsqrt(fma(E, E, 4.0 * r2));
+      cs = c2(E * h, sg * 2.0 * r * h);
+      e = c2(bv.x * rinv, bv.y * rinv);
+      shift = sg * 2.0 * r2 / (E * sc);
+    }
+  }
+  // The same rotation with the hardware reciprocal square root / reciprocal
+  // plus one Newton-type refinement each (inputs kept in the normal range by
+  // the rescale), branch-free apart from the rare rescale: ~40 instructions
+  // instead of ~90 for the IEEE sqrt / division expansions.
+  __device__ __forceinline__ static double rsq_ref(double x) {  // x > 0 normal
+    const double y = __builtin_amdgcn_rsq(x);
+    const double d = fma(-x * y, y, 1.0);  // 1 - x y^2
+    return fma(y * d, fma(d, 0.375, 0.5), y);
+  }
+  __device__ __forceinline__ static double rcp_ref(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    return fma(y, fma(-x, y, 1.0), y);
+  }
+  __device__ __forceinline__ static void jrot_fast(zc bv, double app, double aqq, zc& cs, zc& e, double& shift) {
+    double r2 = bv.x * bv.x + bv.y * bv.y;
+    const bool need = jneed(r2, app, aqq);
+    double sc = 1.0;
+    const double mb = fmax(fabs(bv.x), fabs(bv.y)), sz = fabs(app) + fabs(aqq);
+    if (need && (mb < 1e-120 || mb > 1e120 || sz > 1e120)) {
+      sc = ldexp(1.0, -ilogb(fmax(mb, sz)));
+      bv = cscale(bv, sc); app *= sc; aqq *= sc;
+      r2 = bv.x * bv.x + bv.y * bv.y;
+    }
+    const double rinv = rsq_ref(r2), r = r2 * rinv;
+    const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
+    const double x = fma(D, D, 4.0 * r2);
+    const double E = fabs(D) + x * rsq_ref(x);
+    const double h = rsq_ref(fma(E, E, 4.0 * r2));
+    cs = need ? c2(E * h, sg * 2.0 * r * h) : c2(1.0, 0.0);
+    e = need ? c2(bv.x * rinv, bv.y * rinv) : c2(1.0, 0.0);
+    shift = need ? sg * 2.0 * r2 * rcp_ref(E * sc) : 0.0;
+  }
   __device__ __forceinline__ void jrot(const JP& d, int t, int rnd, lzp Gc) {
     if (d.n == 0) return;
     const int M = d.m - 1, n = d.n;
@@ -670,26 +726,7 @@ struct Chain {
       const int pp_ = a < b ? a : b, qq_ = a < b ? b : a;
       if (qq_ < n) {
         lzp g = Gc + d.go;
-        zc bv = g[pp_ * n + qq_];
-        double app = zc(g[pp_ * n + pp_]).x, aqq = zc(g[qq_ * n + qq_]).x;
-        double r2 = bv.x * bv.x + bv.y * bv.y;
-        if (jneed(r2, app, aqq)) {
-          // power-of-two rescale keeps r^2 and D^2 in range (exact, rare)
-          double sc = 1.0;
-          const double mb = fmax(fabs(bv.x), fabs(bv.y)), sz = fabs(app) + fabs(aqq);
-          if (mb < 1e-120 || mb > 1e120 || sz > 1e120) {
-            sc = ldexp(1.0, -ilogb(fmax(mb, sz)));
-            bv = cscale(bv, sc); app *= sc; aqq *= sc;
-            r2 = bv.x * bv.x + bv.y * bv.y;
-          }
-          const double rinv = rsqrt(r2), r = r2 * rinv;
-          const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
-          const double E = fabs(D) + sqrt(fma(D, D, 4.0 * r2));
-          const double h = rsqrt(fma(E, E, 4.0 * r2));
-          cs = c2(E * h, sg * 2.0 * r * h);
-          e = c2(bv.x * rinv, bv.y * rinv);
-          shift = sg * 2.0 * r2 / (E * sc);
-        }
+        jrot_val(g[pp_ * n + qq_], zc(g[pp_ * n + pp_]).x, zc(g[qq_ * n + qq_]).x, cs, e, shift);
       }
     }
     ROT[2 * t] = cs;
@@ -806,12 +843,125 @@ struct Chain {
   // all rounds (JB_IT x NT elements, JA_IT x NT pairs; larger problems fall
   // back to per-round lookups).  Convergence is tested on the output of each
   // sweep's last round.  On exit Gc/Wc point at the converged buffers.
+  // Register-resident Jacobi for decompositions whose blocks all have order
+  // m <= S (S = 4 or 8): block b lives in one S*S-lane group of a wave (lane
+  // S*i + j holds G[i][j] and W[i][j]; padding lanes hold zeros).  Per round
+  // the lane holding the pivot g[p][q] (p < q paired this round) evaluates
+  // the rotation (jrot_val, the phase-A formula); every lane then gathers the
+  // rotations of its column pair and row pair and the three partner elements
+  // of its 2x2 super-block with ds_bpermute and applies the phase-B update
+  // (jupd_fast).  Same pairing, formulas and sweep structure as the LDS path,
+  // but no block barrier: a wave sweeps its own blocks until its convergence
+  // ballot is empty (sweeps over converged blocks are exact no-ops, so
+  // per-wave termination changes nothing).  Writes G and W back in place;
+  // the caller syncs.
+  __device__ __forceinline__ static double bperm(double v, int addr) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, int(b)), hi = __builtin_amdgcn_ds_bpermute(addr, int(b >> 32));
+    return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+  }
+  __device__ __forceinline__ static zc bpermz(zc v, int addr) { return c2(bperm(v.x, addr), bperm(v.y, addr)); }
+  template <int S>
+  __device__ OCG_INLINE void jacobi_reg(lzp Gc, lzp Wc, int maxr) {
+    constexpr int GS = S * S;     // lanes per block
+    constexpr int BPW = 64 / GS;  // blocks per wave
+    const int Q1 = P.Q1;
+    const int i = (lane / S) % S, j = lane % S, rb = lane & ~(GS - 1);
+    const int wave = tid >> 6;
+    auto at = [&](int r, int c) { return (rb + r * S + c) << 2; };  // bpermute byte address of (r, c)
+    for (int b0 = wave * BPW; b0 < Q1; b0 += BPW * NW) {
+      const int q = b0 + lane / GS;
+      const bool blk_ok = q < Q1;
+      const int n = blk_ok ? NQ[q] : 0, m = blk_ok ? MQ[q] : 0, go = blk_ok ? GOFF[q] : 0;
+      const bool valid = i < n && j < n;
+      const int loc = go + i * n + j;
+      zc g = valid ? zc(Gc[loc]) : c2(0.0, 0.0);
+      zc w = valid ? zc(Wc[loc]) : c2(i == j ? 1.0 : 0.0, 0.0);
+      // partners of i and j in every round (3 bits each; idle / padded: self)
+      int pti = 0, ptj = 0;
+      for (int rnd = 0; rnd < maxr; ++rnd) {
+        int pi = i, pj = j, t;
+        if (i < n && jpair(i, rnd, m, n, t) >= 0) pi = t;
+        if (j < n && jpair(j, rnd, m, n, t) >= 0) pj = t;
+        pti |= pi << (3 * rnd);
+        ptj |= pj << (3 * rnd);
+      }
+      int sweep = 0;
+      for (; sweep < 40; ++sweep) {
+        bool flag = false;
+        for (int rnd = 0; rnd < maxr; ++rnd) {
+          const int pi = (pti >> (3 * rnd)) & 7, pj = (ptj >> (3 * rnd)) & 7;
+          // pivot lanes: rotation of pair (i, j)
+          const double dpp = bperm(g.x, at(i, i)), dqq = bperm(g.x, at(j, j));
+          zc cs, e;
+          double sh;
+          jrot_fast(g, dpp, dqq, cs, e, sh);
+          const bool piv = i < j && pi == j;
+          cs = piv ? cs : c2(1.0, 0.0);
+          sh = piv ? sh : 0.0;
+          // rotations of the column pair (j, pj) and the row pair (i, pi)
+          const int aj = at(j < pj ? j : pj, j < pj ? pj : j), ai = at(i < pi ? i : pi, i < pi ? pi : i);
+          const zc csj = bpermz(cs, aj), ej = bpermz(e, aj), csi = bpermz(cs, ai), ei = bpermz(e, ai);
+          const double shj = bperm(sh, aj);
+          const zc g01 = bpermz(g, at(i, pj)), g10 = bpermz(g, at(pi, j)), g11 = bpermz(g, at(pi, pj));
+          const zc w1 = bpermz(w, at(i, pj));
+          const bool rotj = pj != j && csj.y != 0.0, roti = pi != i && csi.y != 0.0;
+          zc jjj, jpj, jii, jpi;
+          jcol(j < pj, csj, ej, jjj, jpj);
+          jcol(i < pi, csi, ei, jii, jpi);
+          jjj = rotj ? jjj : c2(1, 0);
+          jpj = rotj ? jpj : c2(0, 0);
+          jii = roti ? jii : c2(1, 0);
+          jpi = roti ? jpi : c2(0, 0);
+          zc wn = cmul(w, jjj);
+          cacc(wn, w1, jpj);
+          zc r0 = cmul(g, jjj);
+          cacc(r0, g01, jpj);
+          zc r1 = cmul(g10, jjj);
+          cacc(r1, g11, jpj);
+          zc out = cjmul(jii, r0);
+          cjacc(out, jpi, r1);
+          const bool zero = rotj && roti && pi == j;
+          const bool diag = rotj && i == j;
+          out = zero ? c2(0, 0) : out;
+          out = diag ? c2(g.x + (j < pj ? -shj : shj), 0) : out;
+          if (rnd == maxr - 1)  // convergence: the rotation predicate on the sweep's output
+            flag = valid && i < j && jneed(cabs2(out), dpp, dqq);
+          g = out;
+          w = wn;
+        }
+        if (__ballot(flag) == 0) break;
+      }
+#ifdef OCG_PROFILE
+      if (tid == 0) { PROF[20] += sweep + 1; PROF[21] += 1.0; PROF[22] += maxr; }  // sweeps, calls, rounds/sweep
+#endif
+      if (valid) {
+        Gc[loc] = g;
+        Wc[loc] = w;
+      }
+    }
+  }
+
   __device__ OCG_INLINE void jacobi(lzp& Gc, lzp& Wc) {
     constexpr int JB_IT = 4, JA_IT = 2;
     lzp Gn = (Gc == G) ? G2 : G;
     lzp Wn = (Wc == W) ? W2 : W;
     const int maxr = ISCAL[I_MAXROUNDS];
     if (maxr <= 0) return;
+#ifndef OCG_NO_REG_JACOBI
+    if (maxr <= 3) {  // every block of order <= 4
+      pf(13);
+      jacobi_reg<4>(Gc, Wc, maxr);
+      sync();
+      return;
+    }
+    if (maxr <= 7) {  // every block of order <= 8
+      pf(13);
+      jacobi_reg<8>(Gc, Wc, maxr);
+      sync();
+      return;
+    }
+#endif
     const int npair = POFF[P.Q1];
     const int nel = GOFF[P.Q1];
     JD dB[JB_IT];

@@ -108,3 +108,7 @@ inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 #define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))
 #define __builtin_amdgcn_fence(o, s) __atomic_thread_fence(__ATOMIC_SEQ_CST)
 #define __builtin_amdgcn_wave_barrier() emu_wbar->arrive_and_wait()
+inline int emu_bpermute(int addr, int v) { return emu_xchg(v, (addr >> 2) & 63); }
+#define __builtin_amdgcn_ds_bpermute(a, v) emu_bpermute((a), (v))
+inline double emu_rsq(double x) { return 1.0 / std::sqrt(x); }
+#define __builtin_amdgcn_rsq(x) emu_rsq(x)

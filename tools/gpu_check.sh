@@ -8,4 +8,4 @@ make -s -C oracle &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo "smoke ok" &&
 timeout -k 10 600 python -m pytest tests -m gpu -x -q -rf --tb=short > gpurun_out/pytest.log 2>&1 && echo "pytest ok" &&
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 && echo "bench ok" &&
-timeout -k 10 300 python tools/profile_phases.py > gpurun_out/phases.log 2>&1 && echo "phases ok"
+timeout -k 10 300 python tools/time_parts.py > gpurun_out/parts.log 2>&1 && echo "parts ok"
