@@ -887,12 +887,20 @@ struct Chain {
         ptj |= pj << (3 * rnd);
       }
       int sweep = 0;
+      bool done = false;
       for (; sweep < 40; ++sweep) {
         bool flag = false;
         for (int rnd = 0; rnd < maxr; ++rnd) {
           const int pi = (pti >> (3 * rnd)) & 7, pj = (ptj >> (3 * rnd)) & 7;
           // pivot lanes: rotation of pair (i, j)
           const double dpp = bperm(g.x, at(i, i)), dqq = bperm(g.x, at(j, j));
+          // early exit: no pair of the wave's blocks passes the rotation
+          // predicate, so the rest of this sweep is a chain of exact no-ops
+          // and the end-of-sweep test would stop after it (same result)
+          if (__ballot(valid && i < j && jneed(cabs2(g), dpp, dqq)) == 0) {
+            done = true;
+            break;
+          }
           zc cs, e;
           double sh;
           jrot_fast(g, dpp, dqq, cs, e, sh);
@@ -930,7 +938,7 @@ struct Chain {
           g = out;
           w = wn;
         }
-        if (__ballot(flag) == 0) break;
+        if (done || __ballot(flag) == 0) break;
       }
 #ifdef OCG_PROFILE
       if (tid == 0) { PROF[20] += sweep + 1; PROF[21] += 1.0; PROF[22] += maxr; }  // sweeps, calls, rounds/sweep

@@ -143,8 +143,8 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
 // exists instead of after both trajectory sweeps, and the <xiH_j|psiH_i(j)>
 // overlaps move to a second, fully parallel kernel:
 //   k_pipeline   grid [0] psi chain, [1] xi chain (each publishes state t via
-//                flags[t] / flags[N+t]), [2, 2+N) xiH_t = dH xi_t,
-//                [2+N, 2+N+nrows) row r: wait psi_i, psiH = dH psi_i, store
+//                flags[t] / flags[N+t]), [2, 2+nxw) xiH_t = dH xi_t workers,
+//                [2+nxw, 2+nxw+nrows) row r: wait psi_i, psiH = dH psi_i, store
 //                psiH_i(i..N-2) (the states calcHessianRow overlaps, :251-279)
 //   k_row_overlaps  one workgroup per stored psiH_i(j): overlap with xiH_j, H_ij
 // Producers and consumers live in one grid; consumers only ever wait on
@@ -181,7 +181,7 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
                                          Pool pool, int slot_init, int slot_target, int psi_base, int xi_base,
                                          int xih_base, const double* u, int N, const int* rows, int nrows,
                                          const int* rbase, Pool rs, double* rnorm, int* flags, int epoch, int* err,
-                                         double* stats) {
+                                         int nxw, double* stats) {
   Chain<NT> c(P, smem);
   c.load_tables(gf, gb, md);
   const int b = blockIdx.x;
@@ -204,15 +204,18 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
       t = tn;
     }
     nsteps = N - 1;
-  } else if (b < 2 + N) {
-    // xiHlist[t] = exactApplyMPO(propDeriv, xi_t[t]) (:300-303)
-    const int t = b - 2;
-    if (!await_flag(c, flags + N + t, epoch, err)) return;
-    c.load(SLOT_D(pool, P, xi_base + t), SLOT_X(pool, P, xi_base + t));
-    c.apply_dH();
-    c.store(SLOT_D(pool, P, xih_base + t), SLOT_X(pool, P, xih_base + t));
+  } else if (b < 2 + nxw) {
+    // xiHlist[t] = exactApplyMPO(propDeriv, xi_t[t]) (:300-303): nxw workers
+    // take t = N-1-w, N-1-w-nxw, ... in the order the xi chain publishes
+    // them, so few workgroups keep up with it and every row keeps a CU
+    for (int t = N - 1 - (b - 2); t >= 0; t -= nxw) {
+      if (!await_flag(c, flags + N + t, epoch, err)) return;
+      c.load(SLOT_D(pool, P, xi_base + t), SLOT_X(pool, P, xi_base + t));
+      c.apply_dH();
+      c.store(SLOT_D(pool, P, xih_base + t), SLOT_X(pool, P, xih_base + t));
+    }
   } else {
-    const int r = b - 2 - N;
+    const int r = b - 2 - nxw;
     if (r >= nrows) return;
     const int i = rows[r];
     if (!await_flag(c, flags + i, epoch, err)) return;

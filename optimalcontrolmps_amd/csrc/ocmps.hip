@@ -29,6 +29,7 @@ static inline zc mkz(double x, double y) { zc r; r.x = x; r.y = y; return r; }
 #define OCG_NT 128
 #endif
 static constexpr int NT = OCG_NT;
+static constexpr int kXiHWorkers = 8;
 
 #include "kernels.hpp"
 using ocg::Pool;
@@ -69,10 +70,10 @@ __global__ __launch_bounds__(NT) void k_pipeline(OcgParams P, const zc* gf, cons
                                                  int slot_init, int slot_target, int psi_base, int xi_base,
                                                  int xih_base, const double* u, int N, const int* rows, int nrows,
                                                  const int* rbase, Pool rs, double* rnorm, int* flags, int epoch,
-                                                 int* err, double* stats) {
+                                                 int* err, int nxw, double* stats) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_pipeline<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, xih_base, u, N, rows,
-                         nrows, rbase, rs, rnorm, flags, epoch, err, stats);
+                         nrows, rbase, rs, rnorm, flags, epoch, err, nxw, stats);
 }
 
 __global__ __launch_bounds__(NT) void k_row_overlaps(OcgParams P, const zc* gf, const zc* gb, const int* md,
@@ -740,9 +741,12 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   const int* d_rows = c->d_rows;
   const int* d_rbase = c->d_rows + nrows;
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_pipeline, dim3(2 + N + nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb,
+  // xiH workers: the xi chain publishes one state per step and one dH
+  // application costs about one step, so a few workers keep up
+  const int nxw = std::min(N, kXiHWorkers);
+  hipLaunchKernelGGL(k_pipeline, dim3(2 + nxw + nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb,
                      c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->xih_base(),
-                     c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err,
+                     c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err, nxw,
                      c->d_stats + 5 * 3);
   if (int rc = end_kernel(c, 5)) return rc;
   int err = 0;

@@ -234,9 +234,10 @@ void emu_hessian_fused(void* h, const int* dt_, const double* tgt, const int* di
   std::vector<double> rn(nrows, 0.0);
   std::vector<int> flags(2 * N, 0);
   int err = 0;
-  launch(e, 2 + N + nrows, [&](char* smem) {
+  const int nxw = N < 8 ? N : 8;
+  launch(e, 2 + nxw + nrows, [&](char* smem) {
     ocg::body_pipeline<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, xih, u, N, rows.data(),
-                           nrows, rb.data(), rs, rn.data(), flags.data(), 1, &err, e.stats);
+                           nrows, rb.data(), rs, rn.data(), flags.data(), 1, &err, nxw, e.stats);
   });
   std::vector<int> xs(N), ys(N);
   std::vector<ocg::zc> pc(N + 1);

@@ -3,10 +3,14 @@ import os, sys, subprocess, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 NT = int(os.environ.get("OCG_PROF_NT", "64"))
-lib = f"/tmp/libocg_prof{NT}.so"
-subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                       "-DOCG_PROFILE", f"-DOCG_NT={NT}", "-o", lib,
-                       os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip")])
+lib = os.path.join(ROOT, "tools", "build", f"libocg_prof{NT}.so")
+if not os.path.exists(lib) or "--rebuild" in sys.argv:  # build on the CPU side before a GPU call
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                           "-DOCG_PROFILE", f"-DOCG_NT={NT}", "-o", lib,
+                           os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip")])
+if "--build-only" in sys.argv:
+    sys.exit(0)
 print(f"NT = {NT}")
 os.environ["OCG_LIB"] = lib
 import numpy as np
