@@ -36,6 +36,9 @@ struct OcgParams {
   int glo[OCG_MAXD], gsz[OCG_MAXD], goff[OCG_MAXD];  // per-Δ gate blocks
   int gtotal;               // complex entries of one direction's gate table
   int lds_bytes;            // dynamic LDS of one chain workgroup
+  int th2cap;               // two-site Θ elements bound (physical bonds)
+  int nplan;                // decomposition plan slots in LDS (0: plans off)
+  int plan_pe;              // Θ elements a plan slot can describe
 };
 
 // Truncation used for gauge moves and the left-to-right half of the dH

@@ -155,9 +155,44 @@ struct LdsLayout {
   // int buffers (offsets in ints, after the double region)
   int DIMS, DIMX, MD, BOFF, BOFFT, TRO, TCO, THR, THC, THO, NQ, SIDE, GOFF, EOFF, MQ, POFF, KEPT, XOFF, YOFF, QST,
       CDIM, COLD, COFF, EQ, RANK, JB, KIDX, PT, ISCAL;
+  int PLAN;  // P.nplan plan slots of plan_layout(P).stride ints
   int nint;
   int bytes;
 };
+
+// ---------------------------------------------------------------- plans
+// A step runs the same sequence of two-site decompositions every time, and
+// the block structure each one sees (the bond dimensions of the MPS at that
+// point) rarely changes from one step to the next.  A plan slot per gate
+// caches that structure: the Θ tables and, per Θ element, the operand
+// offsets of the A_{i1} A_{i2} contraction (BT) and of the gate application
+// (GA).  A step whose dims match the slot's key reuses them instead of
+// rebuilding the tables and searching them element by element (the results
+// are bitwise the same: only index arithmetic is cached).
+// Slot (ints): [0] valid, [1] Θ elements, [KEY] dims key (nsq), Θ tables
+// TRO/TCO (SEG1 each) and THR/THC/THO (Q1P each), BT (2 per element:
+// x1 | x2 << 16, dm | drc << 16), GA (GAW per element: gate row | sz << 16 |
+// lo << 20 | a1 << 24 | a2 << 28, then the sz TH offsets as 16-bit pairs).
+struct PlanLayout {
+  int KEY, TRO, TCO, THR, THC, THO, BT, GA, GAW, stride;
+};
+__host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
+  PlanLayout l;
+  const int SEG1 = P.Q1 * P.p + 1, Q1P = (P.Q1 + 1 + 7) & ~7;
+  auto al = [](int x) { return (x + 3) & ~3; };
+  int i = 4;
+  l.KEY = i; i = al(i + P.nsq);
+  l.TRO = i; i = al(i + SEG1);
+  l.TCO = i; i = al(i + SEG1);
+  l.THR = i; i += Q1P;
+  l.THC = i; i += Q1P;
+  l.THO = i; i += Q1P;
+  l.BT = i; i = al(i + 2 * P.plan_pe);
+  l.GAW = 1 + (P.p + 1) / 2;
+  l.GA = i; i = al(i + l.GAW * P.plan_pe);
+  l.stride = i;
+  return l;
+}
 
 __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   LdsLayout l;
@@ -218,6 +253,7 @@ __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   l.KIDX = i; i = al(i + P.evcap);
   l.PT = i; i = al(i + kPairTable);
   l.ISCAL = i; i += 16;
+  l.PLAN = i; i += P.nplan > 0 ? P.nplan * plan_layout(P).stride : 0;
   l.nint = i;
   l.bytes = l.ncplx * 16 + l.ndbl * 8 + l.nint * 4;
   return l;
@@ -240,6 +276,10 @@ struct Chain {
   LDS double *LAM, *PP, *SH, *RED, *SCAL, *PROF;
   LDS int *DIMS, *DIMX, *MD, *BOFF, *BOFFT, *TRO, *TCO, *THR, *THC, *THO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT,
       *XOFF, *YOFF, *QST, *CDIM, *COLD, *COFF, *EQ, *RANK, *JB, *KIDX, *PT, *ISCAL;
+  LDS int *PLN, *ps = nullptr;  // plan slots; the current decomposition's slot
+  LDS int *TRO0, *TCO0, *THR0, *THC0, *THO0;  // scratch Θ tables (no plan)
+  PlanLayout pl;
+  bool phit = false;  // the current slot's key matched (uniform)
   unsigned long long pf_last = 0;
   int pf_cur = 0;
   // algorithmic-traffic model accumulators (per lane, summed at the end)
@@ -260,6 +300,35 @@ struct Chain {
     KEPT = ib + l.KEPT; XOFF = ib + l.XOFF; YOFF = ib + l.YOFF; QST = ib + l.QST; EQ = ib + l.EQ; RANK = ib + l.RANK;
     JB = ib + l.JB; KIDX = ib + l.KIDX; PT = ib + l.PT; CDIM = ib + l.CDIM; COLD = ib + l.COLD; COFF = ib + l.COFF;
     ISCAL = ib + l.ISCAL;
+    PLN = ib + l.PLAN;
+    pl = plan_layout(P);
+    TRO0 = TRO; TCO0 = TCO; THR0 = THR; THC0 = THC; THO0 = THO;
+  }
+
+  // ------------------------------------------------------------- plans
+  // Bind the Θ tables to plan slot s and test its key against the current
+  // dims (each wave decides alone from LDS that is stable here, so no
+  // barrier).  s < 0 or plans off: scratch tables, no plan.
+  __device__ __forceinline__ void plan_begin(int s) {
+    phit = false;
+    if (s < 0 || s >= P.nplan) { plan_end(); return; }
+    ps = PLN + s * pl.stride;
+    TRO = ps + pl.TRO; TCO = ps + pl.TCO; THR = ps + pl.THR; THC = ps + pl.THC; THO = ps + pl.THO;
+    bool diff = false;
+    for (int i = lane; i < P.nsq; i += 64) diff |= DIMS[i] != ps[pl.KEY + i];
+    phit = ps[0] != 0 && __ballot(diff) == 0;
+  }
+  __device__ __forceinline__ void plan_end() {
+    ps = nullptr;
+    phit = false;
+    TRO = TRO0; TCO = TCO0; THR = THR0; THC = THC0; THO = THO0;
+  }
+  // after a miss: the slot now describes the current dims (called after the
+  // phases that filled it, before the dims change; read again next step)
+  __device__ __forceinline__ void plan_commit(int tot) {
+    if (!ps || phit) return;
+    for (int i = tid; i < P.nsq; i += NT) ps[pl.KEY + i] = DIMS[i];
+    if (tid == 0) { ps[1] = tot; ps[0] = (tot <= P.plan_pe) ? 1 : 0; }
   }
 
   __device__ __forceinline__ void sync() { __syncthreads(); }
@@ -441,6 +510,7 @@ struct Chain {
   // directions out of every decomposition (guards the LDS capacities).
   __device__ OCG_INLINE void load_tables(const zc* gf, const zc* gb, const int* md) {
     for (int i = tid; i < 32; i += NT) PROF[i] = 0.0;
+    for (int s = tid; s < P.nplan; s += NT) PLN[s * pl.stride] = 0;  // no plan is valid yet
     // circle-method pairing table (see jpair)
     for (int e = tid; e < kPairTable; e += NT) {
       int m = 2;
@@ -496,12 +566,18 @@ struct Chain {
   // ------------------------------------------------------------- Θ
   // Two-site tensor for bond (i1, i1+1), blocks by middle QN q:
   //   rows (n1, a in bond i1-1 sector q-n1), cols (n2, c in bond i1+1 sector q+n2)
-  __device__ OCG_INLINE void build_theta(int i1) {
+  __device__ OCG_INLINE void build_theta(int i1, int slot = -1) {
     pf(0);
     const int l = i1 - 1, mid = i1, r = i1 + 1;
-    pf(15);
-    const int tot = theta_tables([&](int q, int n) { return d(l, q - n); },
-                                 [&](int q, int n) { return d(r, q + n); });
+    plan_begin(slot);
+    int tot;
+    if (phit) {
+      tot = ps[1];
+      if (tid == 0) ISCAL[I_THT] = tot;
+    } else {
+      pf(15);
+      tot = theta_tables([&](int q, int n) { return d(l, q - n); }, [&](int q, int n) { return d(r, q + n); });
+    }
     pf(0);
         // traffic model of this two-site update
     if (w0) {
@@ -511,6 +587,21 @@ struct Chain {
       }
       if (lane == 0) m_bytes += 16.0 * (2.0 * (site_used(i1) + site_used(r)) + P.gtotal);
     }
+    if (phit) {
+      const LDS int* bt = ps + pl.BT;
+      for (int e = tid; e < tot; e += NT) {
+        const int w0_ = bt[2 * e], w1_ = bt[2 * e + 1];
+        const int dm = w1_ & 0xffff, drc = (unsigned)w1_ >> 16;
+        lzp X1 = A + (w0_ & 0xffff);
+        lzp X2 = A + ((unsigned)w0_ >> 16);
+        zc acc = c2(0, 0);
+        for (int b = 0; b < dm; ++b) cacc(acc, X1[b], X2[b * drc]);
+        TH[e] = acc;
+      }
+      sync();
+      return;
+    }
+    const bool rec = ps != nullptr;
     for (int base = 0; base < tot; base += NT) {
       const int e = base + tid;
       const int q = blk(THO, e);
@@ -523,13 +614,20 @@ struct Chain {
         const int ia = row - o1, ic = col - o2;
         const int dm = d(mid, q);
         zc acc = c2(0, 0);
+        int x1 = 0, x2 = 0, drc = 0;
         if (dm > 0) {
-          lzp X1 = site(i1) + bo(i1, q - n1, n1) + ia * dm;
-          const int drc = d(r, q + n2);
-          lzp X2 = site(r) + bo(r, q, n2) + ic;
+          x1 = P.site_base[i1] + bo(i1, q - n1, n1) + ia * dm;
+          drc = d(r, q + n2);
+          x2 = P.site_base[r] + bo(r, q, n2) + ic;
+          lzp X1 = A + x1;
+          lzp X2 = A + x2;
           for (int b = 0; b < dm; ++b) cacc(acc, X1[b], X2[b * drc]);
         }
         TH[e] = acc;
+        if (rec && e < P.plan_pe) {
+          ps[pl.BT + 2 * e] = x1 | (x2 << 16);
+          ps[pl.BT + 2 * e + 1] = dm | (drc << 16);
+        }
       }
     }
     sync();
@@ -546,7 +644,30 @@ struct Chain {
     lzp UF = PH;
     lzp UT = PH + p;
     const int tot = ISCAL[I_THT];
-        for (int base = 0; base < tot; base += NT) {
+    if (phit) {
+      const LDS int* ga = ps + pl.GA;
+      for (int e = tid; e < tot; e += NT) {
+        const LDS int* gd = ga + e * pl.GAW;
+        const unsigned h = gd[0];
+        const int sz = (h >> 16) & 15, lo = (h >> 20) & 15, a1 = (h >> 24) & 15, a2 = h >> 28, D = a1 + a2;
+        lzp g = gt + int(h & 0xffff);
+        zc acc = c2(0, 0);
+        for (int x = 0; x < sz; ++x) {
+          const int n1 = lo + x, n2 = D - n1;
+          zc z = TH[(unsigned(gd[1 + (x >> 1)]) >> (16 * (x & 1))) & 0xffff];
+          if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
+          cacc(acc, g[x], z);
+        }
+        if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
+        else if (lonely) acc = cmul(acc, UT[a2]);
+        X[e] = acc;
+      }
+      sync();
+      lzp t = TH; TH = X; X = t;
+      return;
+    }
+    const bool rec = ps != nullptr;
+    for (int base = 0; base < tot; base += NT) {
       const int e = base + tid;
       const int q = blk(THO, e);
       if (e < tot) {
@@ -559,13 +680,22 @@ struct Chain {
         const int D = a1 + a2, ql = q - a1;
         const int lo = P.glo[D], sz = P.gsz[D], y = a1 - lo;
         lzp g = gt + P.goff[D] + y * sz;
+        const bool rr = rec && e < P.plan_pe;
+        LDS int* gd = rr ? ps + pl.GA + e * pl.GAW : nullptr;
+        if (rr) gd[0] = (P.goff[D] + y * sz) | (sz << 16) | (lo << 20) | (a1 << 24) | (a2 << 28);
         zc acc = c2(0, 0);
+        int pk = 0;
         for (int x = 0; x < sz; ++x) {
           const int n1 = lo + x, n2 = D - n1, qs = ql + n1;
           const int ro = TRO[qs * p + n1] - TRO[qs * p], co = TCO[qs * p + n2] - TCO[qs * p];
-          zc z = TH[THO[qs] + (ro + ia) * THC[qs] + co + ic];
+          const int ad = THO[qs] + (ro + ia) * THC[qs] + co + ic;
+          zc z = TH[ad];
           if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
           cacc(acc, g[x], z);
+          if (rr) {
+            pk |= ad << (16 * (x & 1));
+            if ((x & 1) || x + 1 == sz) { gd[1 + (x >> 1)] = pk; pk = 0; }
+          }
         }
         if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
         else if (lonely) acc = cmul(acc, UT[a2]);
@@ -574,6 +704,7 @@ struct Chain {
     }
     sync();
     lzp t = TH; TH = X; X = t;
+    plan_commit(tot);
   }
 
   // ------------------------------------------------------------- Jacobi
@@ -1118,6 +1249,7 @@ struct Chain {
           PP[rk] = lam;
         }
         wsync();
+        pf(18);
         // truncation (ITensor truncate; relative cutoff; floor 1e-30): the
         // discarded set {j >= 1 : j >= maxm or sum_{i>=j} PP[i] < cutoff*total
         // or PP[j] <= 1e-30 total} is a suffix of the sorted spectrum
@@ -1141,6 +1273,7 @@ struct Chain {
         const int ix = wscan(R * kq), iy = wscan(kq * C);
         if (lane < Q1) { KEPT[lane] = kq; XOFF[lane] = ix - R * kq; YOFF[lane] = iy - kq * C; }
         if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; ISCAL[I_M] = m; SCAL[S_TOTAL] = total; SCAL[S_KEPTW] = kw; }
+        pf(19);
         if (ts) {  // two-site update: new bond ts and the layouts of sites ts, ts+1
           if (lane < Q1) DIMS[ts * Q1 + lane] = kq;
           wsync();
@@ -1278,6 +1411,7 @@ struct Chain {
         } else X[e] = out;
       }
     }
+    pf(23);
     for (int base = 0; base < yt; base += NT) {
       const int e = base + tid;
       const int q = blk(YOFF, e);
@@ -1321,7 +1455,8 @@ struct Chain {
     else
       tot = theta_tables([&](int q, int n) { return n == 0 ? d(k - 1, q) : 0; },
                          [&](int q, int n) { return d(k, q + n); });
-        for (int base = 0; base < tot; base += NT) {
+    pf(28);
+    for (int base = 0; base < tot; base += NT) {
       const int e = base + tid;
       const int q = blk(THO, e);
       if (e < tot) {
@@ -1346,7 +1481,7 @@ struct Chain {
   __device__ OCG_INLINE void gauge_right(int k, double cutoff, int maxm) {
     site_to_theta(k, true);
     decompose(kFromleft, cutoff, maxm, false, MD + k * P.Q1);
-    pf(7);
+    pf(24);
     // new layout of site k+1 (rows = new bond k) into BOFFT
     if (w0)
       scan_excl(BOFFT, SEG, [&](int s) {
@@ -1355,6 +1490,7 @@ struct Chain {
         return KEPT[q] * d(k + 1, q + n);
       }, QST);
     sync();
+    pf(25);
     // S = Y * A_{k+1}   (per (q, n): k_q x d(k+1, q+n))
     const int ns = BOFFT[SEG];
     {
@@ -1375,11 +1511,13 @@ struct Chain {
       }
     }
     sync();
+    pf(26);
     if (w0 && lane < P.Q1) DIMS[k * P.Q1 + lane] = KEPT[lane];
     sync();
     if (w0) site_offsets(k);
     for (int i = tid; i <= SEG; i += NT) boff(k + 1)[i] = BOFFT[i];
     sync();
+    pf(27);
     // A_k <- X ; A_{k+1} <- S
     const int xt = XOFF[P.Q1];
     for (int base = 0; base < xt; base += NT) {
@@ -1401,7 +1539,7 @@ struct Chain {
   __device__ OCG_INLINE void gauge_left(int k, double cutoff, int maxm) {
     site_to_theta(k, false);
     decompose(kFromright, cutoff, maxm, false, MD + (k - 1) * P.Q1);
-    pf(7);
+    pf(24);
     // new layout of site k-1 (cols = new bond k-1) into BOFFT
     if (w0)
       scan_excl(BOFFT, SEG, [&](int s) {
@@ -1410,6 +1548,7 @@ struct Chain {
         return (ql + n <= P.Q) ? d(k - 2, ql) * KEPT[ql + n] : 0;
       }, QST);
     sync();
+    pf(25);
     // S = A_{k-1} * X   (per (ql, n): d(k-2, ql) x k_{ql+n})
     const int ns = BOFFT[SEG];
     {
@@ -1430,11 +1569,13 @@ struct Chain {
       }
     }
     sync();
+    pf(26);
     if (w0 && lane < P.Q1) DIMS[(k - 1) * P.Q1 + lane] = KEPT[lane];
     sync();
     if (w0) site_offsets(k);
     for (int i = tid; i <= SEG; i += NT) boff(k - 1)[i] = BOFFT[i];
     sync();
+    pf(27);
     const int yt = YOFF[P.Q1];
     for (int base = 0; base < yt; base += NT) {
       const int e = base + tid;
@@ -1465,6 +1606,7 @@ struct Chain {
   __device__ OCG_INLINE void step(double ufrom, double uto, int forward) {
     const int L = P.L, p = P.p;
     const double tau = forward ? P.dt : -P.dt;
+    pf(29);
     if (tid < p) {
       double nn = double(tid) * double(tid - 1);
       double af = -0.25 * ufrom * tau * nn, at = -0.25 * uto * tau * nn;
@@ -1477,7 +1619,7 @@ struct Chain {
     bool movingFromLeft = true;
     for (int g = 0; g < P.ngates; ++g) {
       const int i1 = P.gate_i1[g], i2 = i1 + 1;
-      build_theta(i1);
+      build_theta(i1, g);
       if (movingFromLeft) apply_gate(i1, forward, 0, (i2 == L && L % 2 == 0) ? 1 : 0);
       else apply_gate(i1, forward, 1, 0);
       // next gate: right of this one -> Fromleft, centre i2, move to ni1;
@@ -1486,6 +1628,7 @@ struct Chain {
       const int ni1 = more ? P.gate_i1[g + 1] : 0, ni2 = ni1 + 1;
       const int dir = (more && ni1 >= i2) ? kFromleft : kFromright;
       decompose(dir, P.cutoff, P.maxm, true, MD + i1 * P.Q1, i1);  // writes sites i1, i2
+      plan_end();
       centre = (dir == kFromleft) ? i2 : i1;
       const int target = !more ? 1 : (dir == kFromleft ? ni1 : ni2);
       position(centre, target);

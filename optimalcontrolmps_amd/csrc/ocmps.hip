@@ -109,6 +109,15 @@ struct KStat {
 struct ocg_ctx {
   int device = 0;
   OcgParams P{};
+  int lds_np = 0;  // LDS of the kernels that never step (no plan slots)
+  // parameter block of those kernels: plans off, smaller LDS
+  OcgParams Pn() const {
+    OcgParams q = P;
+    q.nplan = 0;
+    q.plan_pe = 0;
+    q.lds_bytes = lds_np;
+    return q;
+  }
   double J = 1.0;
   std::vector<int> md;  // (L+1)*Q1 rank bounds
   std::string err;
@@ -325,12 +334,27 @@ static int set_lds(ocg_ctx* c) {
 
 static int finish_params(ocg_ctx* c) {
   if (c->P.gtotal <= 0) return fail(c, OCG_ESTATE, "internal: gate tables must be built before the LDS layout");
+  c->P.nplan = 0;
+  c->P.plan_pe = 0;
   ocg::LdsLayout l = ocg::lds_layout(c->P, NT);
   c->P.lds_bytes = l.bytes;
+  c->lds_np = l.bytes;
   hipDeviceProp_t prop;
   HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
   size_t limit = prop.sharedMemPerBlock;
   if (prop.maxSharedMemoryPerMultiProcessor > limit) limit = prop.maxSharedMemoryPerMultiProcessor;
+  // decomposition plans (one slot per gate) when they fit: 16-bit offsets, LDS
+  if (c->P.cap < 65536 && c->P.thcap < 65536 && c->P.th2cap > 0) {
+    OcgParams q = c->P;
+    q.nplan = q.ngates;
+    q.plan_pe = q.th2cap;
+    const int b = ocg::lds_layout(q, NT).bytes;
+    if (size_t(b) <= limit) {
+      c->P.nplan = q.nplan;
+      c->P.plan_pe = q.plan_pe;
+      c->P.lds_bytes = b;
+    }
+  }
   if (size_t(l.bytes) > limit)
     return fail(c, OCG_ECAP,
                 "chain workgroup needs " + std::to_string(l.bytes) + " B of LDS (> " + std::to_string(limit) +
@@ -494,7 +518,8 @@ static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::ve
   idx.insert(idx.end(), ys.begin(), ys.end());
   HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_overlaps, dim3(n), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+  const OcgParams Pn = c->Pn();
+  hipLaunchKernelGGL(k_overlaps, dim3(n), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                      c->d_idx, c->d_idx + n, n, with_dH, c->d_c, c->d_stats + 1 * 3);
   if (int rc = end_kernel(c, 1)) return rc;
   out.resize(n);
@@ -525,7 +550,8 @@ static int launch_apply_dH(ocg_ctx* c, const std::vector<int>& in, const std::ve
   idx.insert(idx.end(), outs.begin(), outs.end());
   HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_apply_dH, dim3(n), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+  const OcgParams Pn = c->Pn();
+  hipLaunchKernelGGL(k_apply_dH, dim3(n), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                      c->d_idx, c->d_idx + n, n, norms ? c->d_norms : nullptr, c->d_stats + 2 * 3);
   if (int rc = end_kernel(c, 2)) return rc;
   if (norms) HIPCHK(c, hipMemcpy(norms, c->d_norms, sizeof(double) * n, hipMemcpyDeviceToHost));
@@ -655,7 +681,8 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
     in.insert(in.end(), outs.begin(), outs.end());
     HIPCHK(c, hipMemcpyAsync(c->d_idx2, in.data(), sizeof(int) * 2 * nrows, hipMemcpyHostToDevice, c->stream));
     if (int rc = begin_kernel(c)) return rc;
-    hipLaunchKernelGGL(k_apply_dH, dim3(nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+    const OcgParams Pn = c->Pn();
+    hipLaunchKernelGGL(k_apply_dH, dim3(nrows), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md,
                        c->pool, c->d_idx2, c->d_idx2 + nrows, nrows, c->d_rnorm, c->d_stats + 2 * 3);
     if (int rc = end_kernel(c, 2)) return rc;
     // k_apply_dH writes norms[r] (row order); scatter to index i on the host side of the rows kernel
@@ -762,15 +789,17 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * N + 2)) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
     if (int rc = begin_kernel(c)) return rc;
-    hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+    const OcgParams Pn = c->Pn();
+    hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                        c->d_idx, c->d_idx + N, N, 1, c->d_pc, c->d_stats + 1 * 3);
-    hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+    hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                        c->d_idx + 2 * N, c->d_idx + 2 * N + 1, 1, 0, c->d_pc + N, c->d_stats + 1 * 3);
     if (int rc = end_kernel(c, 1)) return rc;
   }
   if (total > 0) {
     if (int rc = begin_kernel(c)) return rc;
-    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb,
+    const OcgParams Pn = c->Pn();
+    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb,
                        c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
                        c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
     if (int rc = end_kernel(c, 6)) return rc;

@@ -128,16 +128,22 @@ inline std::string build_params(OcgParams& P, std::vector<int>& mdv, int L, int 
     cap += s;
     maxsite = std::max(maxsite, s);
   }
-  long long th = 2 * maxsite, ev = 0, ec = 0;
+  long long th = 2 * maxsite, ev = 0, ec = 0, th2 = 0;
   for (int i1 = 1; i1 < L; ++i1) {  // two-site Θ blocks
-    long long t = 0, e = 0;
+    long long t = 0, e = 0, t2 = 0;
     for (int q = 0; q < Q1; ++q) {
-      long long R = 0, C = 0;
-      for (int n = 0; n < p; ++n) { R += md(i1 - 1, q - n); C += md(i1 + 1, q + n); }
+      long long R = 0, C = 0, R2 = 0, C2 = 0;
+      for (int n = 0; n < p; ++n) {
+        R += md(i1 - 1, q - n); C += md(i1 + 1, q + n);
+        if (q - n >= 0) R2 += mdv[(i1 - 1) * Q1 + q - n];
+        if (q + n <= P.Q) C2 += mdv[(i1 + 1) * Q1 + q + n];
+      }
       t += R * C;
+      t2 += R2 * C2;
       e += std::min(R, C);
     }
     th = std::max(th, t);
+    th2 = std::max(th2, t2);
     ev = std::max(ev, e);
   }
   for (int k = 1; k <= L; ++k) {  // single-site and dH zip-up matricisations
@@ -161,6 +167,7 @@ inline std::string build_params(OcgParams& P, std::vector<int>& mdv, int L, int 
   P.cap = int(cap);
   P.max_site_cap = int(maxsite);
   P.thcap = int(th);
+  P.th2cap = int(std::min(th2, th));
   P.ecap = int(ec);
   P.evcap = int(std::max<long long>(ev, 2)) + 2;
   P.nrot = P.evcap + Q1;

@@ -16,8 +16,10 @@ os.environ["OCG_LIB"] = lib
 import numpy as np
 from optimalcontrolmps_amd import ed
 from optimalcontrolmps_amd.native import MPS, Engine
-NAMES = ["build_theta", "apply_gate", "gram", "jacobi", "rank/trunc", "factors", "scatter", "gauge wb", "overlap",
-         "phase/norm", "load/store", "dH zip", "other", "jacobi A", "jacobi B", "theta tabs", "decomp setup"]
+NAMES = {0: "build_theta", 1: "apply_gate", 2: "gram", 3: "jacobi", 4: "rank", 18: "trunc/kept", 19: "ts offsets",
+         5: "factor X", 23: "factor Y", 7: "s2theta tabs", 28: "s2theta copy", 24: "gauge BOFFT", 25: "gauge S",
+         26: "gauge dims", 27: "gauge wb", 8: "overlap", 9: "phase/norm", 10: "load/store", 11: "dH zip", 12: "other",
+         13: "jacobi A", 14: "jacobi B", 15: "theta tabs", 16: "decomp setup", 29: "step phases"}
 L, p, Q, J, dt = 5, 5, 5, 1.0, 0.01
 ini = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, 2.5)[0], L, p, Q))
 tgt = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, 50.0)[0], L, p, Q))
@@ -35,9 +37,9 @@ for what in ["trajectory(2 chains x 200 steps)", "div_t+xi_dH", "hessian_rows(19
         H = eng.hessian_rows(u, list(range(1, 200)), F, d)
     t1 = time.perf_counter()
     pr = eng.profile(True)
-    tot = pr[:17].sum()
+    tot = sum(pr[i] for i in NAMES)
     print(f"== {what}: wall {1e3*(t1-t0):.1f} ms, total cycles {tot:.3e}")
-    for i, n in enumerate(NAMES):
+    for i, n in sorted(NAMES.items()):
         if pr[i] > 0:
             print(f"   {n:12s} {pr[i]:.3e} ({100*pr[i]/tot:5.1f}%)")
     if pr[21] > 0:
