@@ -169,12 +169,22 @@ struct LdsLayout {
 // (GA).  A step whose dims match the slot's key reuses them instead of
 // rebuilding the tables and searching them element by element (the results
 // are bitwise the same: only index arithmetic is cached).
-// Slot (ints): [0] valid, [1] Θ elements, [KEY] dims key (nsq), Θ tables
-// TRO/TCO (SEG1 each) and THR/THC/THO (Q1P each), BT (2 per element:
-// x1 | x2 << 16, dm | drc << 16), GA (GAW per element: gate row | sz << 16 |
-// lo << 20 | a1 << 24 | a2 << 28, then the sz TH offsets as 16-bit pairs).
+// The decomposition's Gram layout (NQ/SIDE/MQ/GOFF/EOFF/POFF) and per-Gram-
+// element operand offsets (GD) follow from the same key.  A second key, the
+// kept dimension per sector (KK), selects the factor layout: XOFF/YOFF, the
+// new offset tables of sites ts, ts+1 (BO1/BO2) and per-factor-element
+// operand / destination offsets (XD, YD).
+// Slot (ints): [0] valid, [1] Θ elements, [2] Jacobi rounds, [3] factor plan
+// valid, [KEY] dims key (nsq), Θ tables TRO/TCO (SEG1 each) and THR/THC/THO
+// (Q1P each), BT (2 per element: x1 | x2 << 16, dm | drc << 16), GA (GAW per
+// element: gate row | sz << 16 | lo << 20 | a1 << 24 | a2 << 28, then the sz
+// TH offsets as 16-bit pairs), Gram tables, GD (2 per element: a | b << 16,
+// stride | len << 12 | side << 24 | diag << 25), KK, XOFF, YOFF, BO1, BO2,
+// XD / YD (4 per element: a | g << 16, dest | len << 16, eoff | j << 16,
+// n | stride << 12 | side << 31).
 struct PlanLayout {
-  int KEY, TRO, TCO, THR, THC, THO, BT, GA, GAW, stride;
+  int KEY, TRO, TCO, THR, THC, THO, BT, GA, GAW, NQ, SIDE, MQ, GOFF, EOFF, POFF, GD, KK, XOFF, YOFF, BO1, BO2, XD, YD,
+      stride;
 };
 __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   PlanLayout l;
@@ -190,6 +200,20 @@ __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   l.BT = i; i = al(i + 2 * P.plan_pe);
   l.GAW = 1 + (P.p + 1) / 2;
   l.GA = i; i = al(i + l.GAW * P.plan_pe);
+  l.NQ = i; i += Q1P;
+  l.SIDE = i; i += Q1P;
+  l.MQ = i; i += Q1P;
+  l.GOFF = i; i += Q1P;
+  l.EOFF = i; i += Q1P;
+  l.POFF = i; i += Q1P;
+  l.GD = i; i = al(i + 2 * P.plan_pe);
+  l.KK = i; i += Q1P;
+  l.XOFF = i; i += Q1P;
+  l.YOFF = i; i += Q1P;
+  l.BO1 = i; i = al(i + SEG1);
+  l.BO2 = i; i = al(i + SEG1);
+  l.XD = i; i = al(i + 4 * P.plan_pe);
+  l.YD = i; i = al(i + 4 * P.plan_pe);
   l.stride = i;
   return l;
 }
@@ -263,7 +287,7 @@ enum { kFromleft = 0, kFromright = 1 };
 
 // scalar slots
 enum { S_TOTAL = 0, S_KEPTW = 1 };
-enum { I_M = 0, I_MAXROUNDS = 1, I_FLAG = 2 /* ..4 */, I_THT = 8 };
+enum { I_M = 0, I_MAXROUNDS = 1, I_FLAG = 2 /* ..4 */, I_THT = 8, I_P2 = 9 };
 
 template <int NT>
 struct Chain {
@@ -277,7 +301,8 @@ struct Chain {
   LDS int *DIMS, *DIMX, *MD, *BOFF, *BOFFT, *TRO, *TCO, *THR, *THC, *THO, *NQ, *SIDE, *GOFF, *EOFF, *MQ, *POFF, *KEPT,
       *XOFF, *YOFF, *QST, *CDIM, *COLD, *COFF, *EQ, *RANK, *JB, *KIDX, *PT, *ISCAL;
   LDS int *PLN, *ps = nullptr;  // plan slots; the current decomposition's slot
-  LDS int *TRO0, *TCO0, *THR0, *THC0, *THO0;  // scratch Θ tables (no plan)
+  LDS int *TRO0, *TCO0, *THR0, *THC0, *THO0;  // scratch tables (no plan)
+  LDS int *NQ0, *SIDE0, *MQ0, *GOFF0, *EOFF0, *POFF0, *XOFF0, *YOFF0;
   PlanLayout pl;
   bool phit = false;  // the current slot's key matched (uniform)
   unsigned long long pf_last = 0;
@@ -303,6 +328,7 @@ struct Chain {
     PLN = ib + l.PLAN;
     pl = plan_layout(P);
     TRO0 = TRO; TCO0 = TCO; THR0 = THR; THC0 = THC; THO0 = THO;
+    NQ0 = NQ; SIDE0 = SIDE; MQ0 = MQ; GOFF0 = GOFF; EOFF0 = EOFF; POFF0 = POFF; XOFF0 = XOFF; YOFF0 = YOFF;
   }
 
   // ------------------------------------------------------------- plans
@@ -314,6 +340,8 @@ struct Chain {
     if (s < 0 || s >= P.nplan) { plan_end(); return; }
     ps = PLN + s * pl.stride;
     TRO = ps + pl.TRO; TCO = ps + pl.TCO; THR = ps + pl.THR; THC = ps + pl.THC; THO = ps + pl.THO;
+    NQ = ps + pl.NQ; SIDE = ps + pl.SIDE; MQ = ps + pl.MQ; GOFF = ps + pl.GOFF; EOFF = ps + pl.EOFF;
+    POFF = ps + pl.POFF; XOFF = ps + pl.XOFF; YOFF = ps + pl.YOFF;
     bool diff = false;
     for (int i = lane; i < P.nsq; i += 64) diff |= DIMS[i] != ps[pl.KEY + i];
     phit = ps[0] != 0 && __ballot(diff) == 0;
@@ -322,13 +350,14 @@ struct Chain {
     ps = nullptr;
     phit = false;
     TRO = TRO0; TCO = TCO0; THR = THR0; THC = THC0; THO = THO0;
+    NQ = NQ0; SIDE = SIDE0; MQ = MQ0; GOFF = GOFF0; EOFF = EOFF0; POFF = POFF0; XOFF = XOFF0; YOFF = YOFF0;
   }
   // after a miss: the slot now describes the current dims (called after the
   // phases that filled it, before the dims change; read again next step)
   __device__ __forceinline__ void plan_commit(int tot) {
     if (!ps || phit) return;
     for (int i = tid; i < P.nsq; i += NT) ps[pl.KEY + i] = DIMS[i];
-    if (tid == 0) { ps[1] = tot; ps[0] = (tot <= P.plan_pe) ? 1 : 0; }
+    if (tid == 0) { ps[1] = tot; ps[0] = (tot <= P.plan_pe) ? 1 : 0; ps[3] = 0; }
   }
 
   __device__ __forceinline__ void sync() { __syncthreads(); }
@@ -1162,7 +1191,15 @@ struct Chain {
                                        int ts = 0) {
     pf(16);
     const int Q1 = P.Q1;
-    if (w0) {
+    if (phit) {  // Gram layout from the plan
+      if (w0) {
+        if (lane < Q1) KEPT[lane] = 0;
+        if (lane == 0) {
+          ISCAL[I_MAXROUNDS] = ps[2];
+          ISCAL[I_FLAG] = 0; ISCAL[I_FLAG + 1] = 0; ISCAL[I_FLAG + 2] = 0;
+        }
+      }
+    } else if (w0) {
       const int q = lane;
       const int R = q < Q1 ? THR[q] : 0, C = q < Q1 ? THC[q] : 0;
       const int n = (R == 0 || C == 0) ? 0 : (R <= C ? R : C);
@@ -1176,13 +1213,30 @@ struct Chain {
       if (lane == 63) {  // inclusive scans: lane 63 holds the totals
         GOFF[Q1] = ig; EOFF[Q1] = ie; POFF[Q1] = ip;
         ISCAL[I_MAXROUNDS] = mr;
+        if (ps) ps[2] = mr;
         ISCAL[I_FLAG] = 0; ISCAL[I_FLAG + 1] = 0; ISCAL[I_FLAG + 2] = 0;
       }
     }
     sync();
     pf(2);
     // Gram matrices and identity eigenvectors
-    {
+    if (phit) {
+      const int nel = GOFF[Q1];
+      const LDS int* gdp = ps + pl.GD;
+      for (int e = tid; e < nel; e += NT) {
+        const unsigned a0 = gdp[2 * e], a1 = gdp[2 * e + 1];
+        const int st = a1 & 0xfff, len = (a1 >> 12) & 0xfff;
+        lzp Ta = TH + int(a0 & 0xffff), Tb = TH + int(a0 >> 16);
+        zc acc = c2(0, 0);
+        if (((a1 >> 24) & 1) == 0) {
+          for (int c = 0; c < len; ++c) cacc(acc, Ta[c * st], cconj(Tb[c * st]));
+        } else {
+          for (int r = 0; r < len; ++r) cjacc(acc, Ta[r * st], Tb[r * st]);
+        }
+        G[e] = acc;
+        W[e] = ((a1 >> 25) & 1) ? c2(1, 0) : c2(0, 0);
+      }
+    } else {
       const int nel = GOFF[Q1];
       for (int base = 0; base < nel; base += NT) {
         const int e = base + tid;
@@ -1201,6 +1255,11 @@ struct Chain {
           }
           G[e] = acc;
           W[e] = (i == j) ? c2(1, 0) : c2(0, 0);
+          if (ps && e < P.plan_pe) {
+            const int o = THO[q], s0 = SIDE[q] == 0;
+            ps[pl.GD + 2 * e] = (s0 ? o + i * C : o + i) | ((s0 ? o + j * C : o + j) << 16);
+            ps[pl.GD + 2 * e + 1] = (s0 ? 1 : C) | ((s0 ? C : R) << 12) | ((s0 ? 0 : 1) << 24) | ((i == j) << 25);
+          }
         }
       }
     }
@@ -1269,16 +1328,41 @@ struct Chain {
           const int c = __popcll(__ballot(kept && q == s));
           kq = (lane == s) ? c : kq;
         }
-        const int R = lane < Q1 ? THR[lane] : 0, C = lane < Q1 ? THC[lane] : 0;
-        const int ix = wscan(R * kq), iy = wscan(kq * C);
-        if (lane < Q1) { KEPT[lane] = kq; XOFF[lane] = ix - R * kq; YOFF[lane] = iy - kq * C; }
-        if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; ISCAL[I_M] = m; SCAL[S_TOTAL] = total; SCAL[S_KEPTW] = kw; }
+        // factor plan: 1 = the slot's factor layout matches kq, 2 = record it
+        int p2 = 0;
+        if (ps && ts) {
+          const bool same = phit && ps[3] != 0 && __ballot(lane < Q1 && ps[pl.KK + lane] != kq) == 0;
+          p2 = same ? 1 : 2;
+        }
+        if (lane < Q1) KEPT[lane] = kq;
+        if (lane == 0) { ISCAL[I_M] = m; SCAL[S_TOTAL] = total; SCAL[S_KEPTW] = kw; ISCAL[I_P2] = p2; }
+        if (p2 != 1) {
+          const int R = lane < Q1 ? THR[lane] : 0, C = lane < Q1 ? THC[lane] : 0;
+          const int ix = wscan(R * kq), iy = wscan(kq * C);
+          if (lane < Q1) { XOFF[lane] = ix - R * kq; YOFF[lane] = iy - kq * C; }
+          if (lane == 63) { XOFF[Q1] = ix; YOFF[Q1] = iy; }
+        }
         pf(19);
         if (ts) {  // two-site update: new bond ts and the layouts of sites ts, ts+1
           if (lane < Q1) DIMS[ts * Q1 + lane] = kq;
-          wsync();
-          site_offsets(ts);
-          site_offsets(ts + 1);
+          if (p2 == 1) {
+            for (int i = lane; i <= SEG; i += 64) {
+              boff(ts)[i] = ps[pl.BO1 + i];
+              boff(ts + 1)[i] = ps[pl.BO2 + i];
+            }
+          } else {
+            wsync();
+            site_offsets(ts);
+            site_offsets(ts + 1);
+            if (p2 == 2) {
+              wsync();
+              for (int i = lane; i <= SEG; i += 64) {
+                ps[pl.BO1 + i] = boff(ts)[i];
+                ps[pl.BO2 + i] = boff(ts + 1)[i];
+              }
+              if (lane < Q1) ps[pl.KK + lane] = kq;
+            }
+          }
         }
       }
       sync();
@@ -1340,7 +1424,7 @@ struct Chain {
           nd += __popcll(__ballot(disc));
           carry += rdlane(inc, 63);
         }
-        if (lane == 0) { ISCAL[I_M] = T - nd; SCAL[S_TOTAL] = total; }
+        if (lane == 0) { ISCAL[I_M] = T - nd; SCAL[S_TOTAL] = total; ISCAL[I_P2] = 0; }
       }
       sync();
       // kept vectors: global rank < m and within the sector's rank bound
@@ -1383,6 +1467,52 @@ struct Chain {
     const double kwv = SCAL[S_KEPTW];
     const double inv = (normalize && kwv > 1e-32) ? 1.0 / sqrt(kwv) : 1.0;
     const int xt = XOFF[Q1], yt = YOFF[Q1];
+    const int pm = ISCAL[I_P2];  // 1: factor plan, 2: record it
+    if (pm == 1) {
+      // X: exact side u = W[a + w], else Θ w (len terms, Θ stride st, W stride n)
+      for (int e = tid; e < xt; e += NT) {
+        const i4 dd = *(const LDS i4*)(ps + pl.XD + 4 * e);
+        const int a = dd[0] & 0xffff, g = unsigned(dd[0]) >> 16, dest = dd[1] & 0xffff, len = unsigned(dd[1]) >> 16;
+        const int eb = dd[2] & 0xffff, j = unsigned(dd[2]) >> 16, n = dd[3] & 0xfff, st = (dd[3] >> 12) & 0x7ffff;
+        const int w = KIDX[eb + j];
+        const double sig = sqrt(LAM[eb + w]);
+        zc out;
+        if (dd[3] < 0) {
+          out = Wc[a + w];
+          if (dir == kFromright) out = cscale(out, sig * inv);
+        } else {
+          zc acc = c2(0, 0);
+          lzp Ta = TH + a, Wg = Wc + g + w;
+          for (int c = 0; c < len; ++c) cacc(acc, Ta[c * st], Wg[c * n]);
+          if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
+          else out = cscale(acc, inv);
+        }
+        A[dest] = out;
+      }
+      pf(23);
+      // Y: exact side v^H = conj(W[a + w]), else w^H Θ
+      for (int e = tid; e < yt; e += NT) {
+        const i4 dd = *(const LDS i4*)(ps + pl.YD + 4 * e);
+        const int a = dd[0] & 0xffff, g = unsigned(dd[0]) >> 16, dest = dd[1] & 0xffff, len = unsigned(dd[1]) >> 16;
+        const int eb = dd[2] & 0xffff, j = unsigned(dd[2]) >> 16, n = dd[3] & 0xfff, st = (dd[3] >> 12) & 0x7ffff;
+        const int w = KIDX[eb + j];
+        const double sig = sqrt(LAM[eb + w]);
+        zc out;
+        if (dd[3] < 0) {
+          out = cconj(Wc[a + w]);
+          if (dir == kFromleft) out = cscale(out, sig * inv);
+        } else {
+          zc acc = c2(0, 0);
+          lzp Ta = TH + a, Wg = Wc + g + w;
+          for (int r = 0; r < len; ++r) cjacc(acc, Wg[r * n], Ta[r * st]);
+          if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
+          else out = cscale(acc, inv);
+        }
+        A[dest] = out;
+      }
+      sync();
+      return;
+    }
     for (int base = 0; base < xt; base += NT) {
       const int e = base + tid;
       const int q = blk(XOFF, e);
@@ -1407,7 +1537,16 @@ struct Chain {
         if (ts) {  // rows (n1, a) of site ts
           int o;
           const int n1 = seg_in(TRO, q, row, o);
-          site(ts)[bo(ts, q - n1, n1) + (row - o) * k + j] = out;
+          const int dest = P.site_base[ts] + bo(ts, q - n1, n1) + (row - o) * k + j;
+          A[dest] = out;
+          if (pm == 2 && e < P.plan_pe) {
+            const bool ex = SIDE[q] == 0;
+            LDS int* dd = ps + pl.XD + 4 * e;
+            dd[0] = (ex ? GOFF[q] + row * n : THO[q] + row * C) | (GOFF[q] << 16);
+            dd[1] = dest | (C << 16);
+            dd[2] = EOFF[q] | (j << 16);
+            dd[3] = n | (1 << 12) | (ex ? int(0x80000000u) : 0);
+          }
         } else X[e] = out;
       }
     }
@@ -1436,11 +1575,21 @@ struct Chain {
         if (ts) {  // cols (n2, c) of site ts+1
           int o;
           const int n2 = seg_in(TCO, q, col, o);
-          site(ts + 1)[bo(ts + 1, q, n2) + j * d(ts + 1, q + n2) + (col - o)] = out;
+          const int dest = P.site_base[ts + 1] + bo(ts + 1, q, n2) + j * d(ts + 1, q + n2) + (col - o);
+          A[dest] = out;
+          if (pm == 2 && e < P.plan_pe) {
+            const bool ex = SIDE[q] == 1;
+            LDS int* dd = ps + pl.YD + 4 * e;
+            dd[0] = (ex ? GOFF[q] + col * n : THO[q] + col) | (GOFF[q] << 16);
+            dd[1] = dest | (R << 16);
+            dd[2] = EOFF[q] | (j << 16);
+            dd[3] = n | (C << 12) | (ex ? int(0x80000000u) : 0);
+          }
         } else Y[e] = out;
       }
     }
     sync();
+    if (pm == 2 && tid == 0) ps[3] = (xt <= P.plan_pe && yt <= P.plan_pe) ? 1 : 0;
   }
 
   // single-site matricisation of site k into TH
