@@ -181,10 +181,13 @@ struct LdsLayout {
 // TH offsets as 16-bit pairs), Gram tables, GD (2 per element: a | b << 16,
 // stride | len << 12 | side << 24 | diag << 25), KK, XOFF, YOFF, BO1, BO2,
 // XD / YD (4 per element: a | g << 16, dest | len << 16, eoff | j << 16,
-// n | stride << 12 | side << 31).
+// n | stride << 12 | exact << 31).  Gauge moves use BT[2e] for the source of
+// each matricised element, BO1 / BO2 for the new offset tables of the
+// neighbour / moved site and SD (4 per element of the neighbour product S:
+// first operand, second operand, length, second stride).
 struct PlanLayout {
   int KEY, TRO, TCO, THR, THC, THO, BT, GA, GAW, NQ, SIDE, MQ, GOFF, EOFF, POFF, GD, KK, XOFF, YOFF, BO1, BO2, XD, YD,
-      stride;
+      SD, stride;
 };
 __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   PlanLayout l;
@@ -214,6 +217,7 @@ __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   l.BO2 = i; i = al(i + SEG1);
   l.XD = i; i = al(i + 4 * P.plan_pe);
   l.YD = i; i = al(i + 4 * P.plan_pe);
+  l.SD = i; i = al(i + 4 * P.plan_pe);
   l.stride = i;
   return l;
 }
@@ -1330,11 +1334,12 @@ struct Chain {
         }
         // factor plan: 1 = the slot's factor layout matches kq, 2 = record it
         int p2 = 0;
-        if (ps && ts) {
+        if (ps) {
           const bool same = phit && ps[3] != 0 && __ballot(lane < Q1 && ps[pl.KK + lane] != kq) == 0;
           p2 = same ? 1 : 2;
         }
         if (lane < Q1) KEPT[lane] = kq;
+        if (p2 == 2 && lane < Q1) ps[pl.KK + lane] = kq;
         if (lane == 0) { ISCAL[I_M] = m; SCAL[S_TOTAL] = total; SCAL[S_KEPTW] = kw; ISCAL[I_P2] = p2; }
         if (p2 != 1) {
           const int R = lane < Q1 ? THR[lane] : 0, C = lane < Q1 ? THC[lane] : 0;
@@ -1360,7 +1365,6 @@ struct Chain {
                 ps[pl.BO1 + i] = boff(ts)[i];
                 ps[pl.BO2 + i] = boff(ts + 1)[i];
               }
-              if (lane < Q1) ps[pl.KK + lane] = kq;
             }
           }
         }
@@ -1487,7 +1491,9 @@ struct Chain {
           if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
-        A[dest] = out;
+        // gauge move (ts = 0): the orthonormal factor goes to its site, the other to scratch
+        if (ts || dir == kFromleft) A[dest] = out;
+        else X[e] = out;
       }
       pf(23);
       // Y: exact side v^H = conj(W[a + w]), else w^H Θ
@@ -1508,7 +1514,8 @@ struct Chain {
           if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
-        A[dest] = out;
+        if (ts || dir == kFromright) A[dest] = out;
+        else Y[e] = out;
       }
       sync();
       return;
@@ -1534,20 +1541,21 @@ struct Chain {
           if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
+        int dest = 0;
         if (ts) {  // rows (n1, a) of site ts
           int o;
           const int n1 = seg_in(TRO, q, row, o);
-          const int dest = P.site_base[ts] + bo(ts, q - n1, n1) + (row - o) * k + j;
+          dest = P.site_base[ts] + bo(ts, q - n1, n1) + (row - o) * k + j;
           A[dest] = out;
-          if (pm == 2 && e < P.plan_pe) {
-            const bool ex = SIDE[q] == 0;
-            LDS int* dd = ps + pl.XD + 4 * e;
-            dd[0] = (ex ? GOFF[q] + row * n : THO[q] + row * C) | (GOFF[q] << 16);
-            dd[1] = dest | (C << 16);
-            dd[2] = EOFF[q] | (j << 16);
-            dd[3] = n | (1 << 12) | (ex ? int(0x80000000u) : 0);
-          }
         } else X[e] = out;
+        if (pm == 2 && e < P.plan_pe) {
+          const bool ex = SIDE[q] == 0;
+          LDS int* dd = ps + pl.XD + 4 * e;
+          dd[0] = (ex ? GOFF[q] + row * n : THO[q] + row * C) | (GOFF[q] << 16);
+          dd[1] = dest | (C << 16);
+          dd[2] = EOFF[q] | (j << 16);
+          dd[3] = n | (1 << 12) | (ex ? int(0x80000000u) : 0);
+        }
       }
     }
     pf(23);
@@ -1572,20 +1580,21 @@ struct Chain {
           if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
+        int dest = 0;
         if (ts) {  // cols (n2, c) of site ts+1
           int o;
           const int n2 = seg_in(TCO, q, col, o);
-          const int dest = P.site_base[ts + 1] + bo(ts + 1, q, n2) + j * d(ts + 1, q + n2) + (col - o);
+          dest = P.site_base[ts + 1] + bo(ts + 1, q, n2) + j * d(ts + 1, q + n2) + (col - o);
           A[dest] = out;
-          if (pm == 2 && e < P.plan_pe) {
-            const bool ex = SIDE[q] == 1;
-            LDS int* dd = ps + pl.YD + 4 * e;
-            dd[0] = (ex ? GOFF[q] + col * n : THO[q] + col) | (GOFF[q] << 16);
-            dd[1] = dest | (R << 16);
-            dd[2] = EOFF[q] | (j << 16);
-            dd[3] = n | (C << 12) | (ex ? int(0x80000000u) : 0);
-          }
         } else Y[e] = out;
+        if (pm == 2 && e < P.plan_pe) {
+          const bool ex = SIDE[q] == 1;
+          LDS int* dd = ps + pl.YD + 4 * e;
+          dd[0] = (ex ? GOFF[q] + col * n : THO[q] + col) | (GOFF[q] << 16);
+          dd[1] = dest | (R << 16);
+          dd[2] = EOFF[q] | (j << 16);
+          dd[3] = n | (C << 12) | (ex ? int(0x80000000u) : 0);
+        }
       }
     }
     sync();
@@ -1597,6 +1606,14 @@ struct Chain {
   //   right (Fromright grouping): rows a in bond k-1 sector q, cols (n, c in bond k sector q+n)
   __device__ OCG_INLINE void site_to_theta(int k, bool left) {
     pf(7);
+    if (phit) {  // plan: source offset of every matricised element
+      pf(28);
+      const int tot = ps[1];
+      const LDS int* bt = ps + pl.BT;
+      for (int e = tid; e < tot; e += NT) TH[e] = A[bt[2 * e]];
+      sync();
+      return;
+    }
     int tot;
     if (left)
       tot = theta_tables([&](int q, int n) { return d(k - 1, q - n); },
@@ -1612,32 +1629,69 @@ struct Chain {
         const int C = THC[q];
         int col, o;
         const int row = udiv(e - THO[q], C, col);
-        zc v;
+        int src;
         if (left) {
           const int n = seg_in(TRO, q, row, o);
-          v = site(k)[bo(k, q - n, n) + (row - o) * C + col];
+          src = bo(k, q - n, n) + (row - o) * C + col;
         } else {
           const int n = seg_in(TCO, q, col, o);
-          v = site(k)[bo(k, q, n) + row * d(k, q + n) + (col - o)];
+          src = bo(k, q, n) + row * d(k, q + n) + (col - o);
         }
-        TH[e] = v;
+        src += P.site_base[k];
+        TH[e] = A[src];
+        if (ps && e < P.plan_pe) ps[pl.BT + 2 * e] = src;
       }
     }
     sync();
+    plan_commit(tot);
   }
 
-  // move the orthogonality centre k -> k+1 (ITensor position, one bond)
-  __device__ OCG_INLINE void gauge_right(int k, double cutoff, int maxm) {
+  // move the orthogonality centre k -> k+1 (ITensor position, one bond).
+  // slot >= 0: plan slot of this gauge move (see plans); on a plan hit the
+  // decomposition writes X straight into site k and the neighbour product
+  // and the new offset tables come from the slot.
+  __device__ OCG_INLINE void gauge_right(int k, double cutoff, int maxm, int slot = -1) {
+    plan_begin(slot);
     site_to_theta(k, true);
     decompose(kFromleft, cutoff, maxm, false, MD + k * P.Q1);
     pf(24);
+    const int pm = ps ? ISCAL[I_P2] : 0;  // 1: plan hit, 2: record
+    if (pm == 1) {
+      pf(25);
+      const int ns = ps[pl.BO1 + SEG];
+      const LDS int* sd = ps + pl.SD;
+      for (int e = tid; e < ns; e += NT) {  // S = Y * A_{k+1}
+        const i4 dd = *(const LDS i4*)(sd + 4 * e);
+        lzp Yq = Y + dd[0];
+        lzp Ab = A + dd[1];
+        zc acc = c2(0, 0);
+        for (int b = 0; b < dd[2]; ++b) cacc(acc, Yq[b], Ab[b * dd[3]]);
+        S[e] = acc;
+      }
+      sync();
+      pf(26);
+      if (w0 && lane < P.Q1) DIMS[k * P.Q1 + lane] = KEPT[lane];
+      for (int i = tid; i <= SEG; i += NT) {
+        boff(k)[i] = ps[pl.BO2 + i];
+        boff(k + 1)[i] = ps[pl.BO1 + i];
+      }
+      for (int e = tid; e < ns; e += NT) site(k + 1)[e] = S[e];
+      sync();
+      plan_end();
+      return;
+    }
     // new layout of site k+1 (rows = new bond k) into BOFFT
-    if (w0)
+    if (w0) {
       scan_excl(BOFFT, SEG, [&](int s) {
         int q, n;
         qn_of(s, q, n);
         return KEPT[q] * d(k + 1, q + n);
       }, QST);
+      if (pm == 2) {
+        wsync();
+        for (int i = lane; i <= SEG; i += 64) ps[pl.BO1 + i] = BOFFT[i];
+      }
+    }
     sync();
     pf(25);
     // S = Y * A_{k+1}   (per (q, n): k_q x d(k+1, q+n))
@@ -1651,11 +1705,16 @@ struct Chain {
           const int cc = d(k + 1, q + n), dold = d(k, q);
           int c;
           const int i = udiv(e - o, cc, c);
-          lzp Yq = Y + YOFF[q] + i * dold;
-          lzp Ab = site(k + 1) + bo(k + 1, q, n) + c;
+          const int yo = YOFF[q] + i * dold, ao = P.site_base[k + 1] + bo(k + 1, q, n) + c;
+          lzp Yq = Y + yo;
+          lzp Ab = A + ao;
           zc acc = c2(0, 0);
           for (int b = 0; b < dold; ++b) cacc(acc, Yq[b], Ab[b * cc]);
           S[e] = acc;
+          if (pm == 2 && e < P.plan_pe) {
+            LDS int* dd = ps + pl.SD + 4 * e;
+            dd[0] = yo; dd[1] = ao; dd[2] = dold; dd[3] = cc;
+          }
         }
       }
     }
@@ -1663,7 +1722,13 @@ struct Chain {
     pf(26);
     if (w0 && lane < P.Q1) DIMS[k * P.Q1 + lane] = KEPT[lane];
     sync();
-    if (w0) site_offsets(k);
+    if (w0) {
+      site_offsets(k);
+      if (pm == 2) {
+        wsync();
+        for (int i = lane; i <= SEG; i += 64) ps[pl.BO2 + i] = boff(k)[i];
+      }
+    }
     for (int i = tid; i <= SEG; i += NT) boff(k + 1)[i] = BOFFT[i];
     sync();
     pf(27);
@@ -1677,25 +1742,64 @@ struct Chain {
         int j, o;
         const int row = udiv(e - XOFF[q], kq, j);
         const int n = seg_in(TRO, q, row, o);
-        site(k)[bo(k, q - n, n) + (row - o) * kq + j] = X[e];
+        const int dest = P.site_base[k] + bo(k, q - n, n) + (row - o) * kq + j;
+        A[dest] = X[e];
+        if (pm == 2 && e < P.plan_pe) {
+          LDS int* dd = ps + pl.XD + 4 * e;
+          dd[1] = (dd[1] & int(0xffff0000u)) | dest;
+        }
       }
     }
     for (int e = tid; e < ns; e += NT) site(k + 1)[e] = S[e];
     sync();
+    if (pm == 2 && tid == 0) ps[3] = (ps[3] != 0 && ns <= P.plan_pe) ? 1 : 0;
+    plan_end();
   }
 
-  // move the orthogonality centre k -> k-1
-  __device__ OCG_INLINE void gauge_left(int k, double cutoff, int maxm) {
+  // move the orthogonality centre k -> k-1 (on a plan hit Y goes straight
+  // into site k)
+  __device__ OCG_INLINE void gauge_left(int k, double cutoff, int maxm, int slot = -1) {
+    plan_begin(slot);
     site_to_theta(k, false);
     decompose(kFromright, cutoff, maxm, false, MD + (k - 1) * P.Q1);
     pf(24);
+    const int pm = ps ? ISCAL[I_P2] : 0;
+    if (pm == 1) {
+      pf(25);
+      const int ns = ps[pl.BO1 + SEG];
+      const LDS int* sd = ps + pl.SD;
+      for (int e = tid; e < ns; e += NT) {  // S = A_{k-1} * X
+        const i4 dd = *(const LDS i4*)(sd + 4 * e);
+        lzp Ab = A + dd[0];
+        lzp Xq = X + dd[1];
+        zc acc = c2(0, 0);
+        for (int b = 0; b < dd[2]; ++b) cacc(acc, Ab[b], Xq[b * dd[3]]);
+        S[e] = acc;
+      }
+      sync();
+      pf(26);
+      if (w0 && lane < P.Q1) DIMS[(k - 1) * P.Q1 + lane] = KEPT[lane];
+      for (int i = tid; i <= SEG; i += NT) {
+        boff(k)[i] = ps[pl.BO2 + i];
+        boff(k - 1)[i] = ps[pl.BO1 + i];
+      }
+      for (int e = tid; e < ns; e += NT) site(k - 1)[e] = S[e];
+      sync();
+      plan_end();
+      return;
+    }
     // new layout of site k-1 (cols = new bond k-1) into BOFFT
-    if (w0)
+    if (w0) {
       scan_excl(BOFFT, SEG, [&](int s) {
         int ql, n;
         qn_of(s, ql, n);
         return (ql + n <= P.Q) ? d(k - 2, ql) * KEPT[ql + n] : 0;
       }, QST);
+      if (pm == 2) {
+        wsync();
+        for (int i = lane; i <= SEG; i += 64) ps[pl.BO1 + i] = BOFFT[i];
+      }
+    }
     sync();
     pf(25);
     // S = A_{k-1} * X   (per (ql, n): d(k-2, ql) x k_{ql+n})
@@ -1709,11 +1813,16 @@ struct Chain {
           const int q = ql + n, kq = KEPT[q], dold = d(k - 1, q);
           int j;
           const int i = udiv(e - o, kq, j);
-          lzp Ab = site(k - 1) + bo(k - 1, ql, n) + i * dold;
-          lzp Xq = X + XOFF[q] + j;
+          const int ao = P.site_base[k - 1] + bo(k - 1, ql, n) + i * dold, xo = XOFF[q] + j;
+          lzp Ab = A + ao;
+          lzp Xq = X + xo;
           zc acc = c2(0, 0);
           for (int b = 0; b < dold; ++b) cacc(acc, Ab[b], Xq[b * kq]);
           S[e] = acc;
+          if (pm == 2 && e < P.plan_pe) {
+            LDS int* dd = ps + pl.SD + 4 * e;
+            dd[0] = ao; dd[1] = xo; dd[2] = dold; dd[3] = kq;
+          }
         }
       }
     }
@@ -1721,7 +1830,13 @@ struct Chain {
     pf(26);
     if (w0 && lane < P.Q1) DIMS[(k - 1) * P.Q1 + lane] = KEPT[lane];
     sync();
-    if (w0) site_offsets(k);
+    if (w0) {
+      site_offsets(k);
+      if (pm == 2) {
+        wsync();
+        for (int i = lane; i <= SEG; i += 64) ps[pl.BO2 + i] = boff(k)[i];
+      }
+    }
     for (int i = tid; i <= SEG; i += NT) boff(k - 1)[i] = BOFFT[i];
     sync();
     pf(27);
@@ -1734,17 +1849,27 @@ struct Chain {
         int col, o;
         const int j = udiv(e - YOFF[q], C, col);
         const int n = seg_in(TCO, q, col, o);
-        site(k)[bo(k, q, n) + j * d(k, q + n) + (col - o)] = Y[e];
+        const int dest = P.site_base[k] + bo(k, q, n) + j * d(k, q + n) + (col - o);
+        A[dest] = Y[e];
+        if (pm == 2 && e < P.plan_pe) {
+          LDS int* dd = ps + pl.YD + 4 * e;
+          dd[1] = (dd[1] & int(0xffff0000u)) | dest;
+        }
       }
     }
     for (int e = tid; e < ns; e += NT) site(k - 1)[e] = S[e];
     sync();
+    if (pm == 2 && tid == 0) ps[3] = (ps[3] != 0 && ns <= P.plan_pe) ? 1 : 0;
+    plan_end();
   }
 
-  __device__ OCG_INLINE void position(int& centre, int target) {
+  // gslot: running index of the step's gauge moves (plan slots follow the
+  // gate slots); null for callers outside a step (no plans)
+  __device__ OCG_INLINE void position(int& centre, int target, int* gslot = nullptr) {
     while (centre != target) {
-      if (centre < target) { gauge_right(centre, OCG_GAUGE_CUTOFF, 1 << 30); ++centre; }
-      else { gauge_left(centre, OCG_GAUGE_CUTOFF, 1 << 30); --centre; }
+      const int slot = gslot ? P.ngates + (*gslot)++ : -1;
+      if (centre < target) { gauge_right(centre, OCG_GAUGE_CUTOFF, 1 << 30, slot); ++centre; }
+      else { gauge_left(centre, OCG_GAUGE_CUTOFF, 1 << 30, slot); --centre; }
     }
   }
 
@@ -1764,7 +1889,7 @@ struct Chain {
     }
     sync();
     if (L % 2 != 0) site_phase(L, PH);  // lonely U_from on site L (:133-136)
-    int centre = 1;
+    int centre = 1, gslot = 0;
     bool movingFromLeft = true;
     for (int g = 0; g < P.ngates; ++g) {
       const int i1 = P.gate_i1[g], i2 = i1 + 1;
@@ -1780,7 +1905,7 @@ struct Chain {
       plan_end();
       centre = (dir == kFromleft) ? i2 : i1;
       const int target = !more ? 1 : (dir == kFromleft ? ni1 : ni2);
-      position(centre, target);
+      position(centre, target, &gslot);
       if (more && (i2 == ni1 || i1 == ni2)) movingFromLeft = false;
     }
     site_phase(1, PH + p);  // lonely U_to on site 1 (:222-223)

@@ -343,16 +343,24 @@ static int finish_params(ocg_ctx* c) {
   HIPCHK(c, hipGetDeviceProperties(&prop, c->device));
   size_t limit = prop.sharedMemPerBlock;
   if (prop.maxSharedMemoryPerMultiProcessor > limit) limit = prop.maxSharedMemoryPerMultiProcessor;
-  // decomposition plans (one slot per gate) when they fit: 16-bit offsets, LDS
-  if (c->P.cap < 65536 && c->P.thcap < 65536 && c->P.th2cap > 0) {
+  // decomposition plans (one slot per decomposition of a step: the gates and
+  // the gauge moves between them) when their 16-bit offsets suffice; the
+  // per-slot element capacity is the two-site / site bound, shrunk to the LDS
+  // left over (a decomposition larger than its slot just runs unplanned)
+  if (c->P.cap < 65536 && c->P.thcap < 65536 && c->P.evcap < 4096) {
     OcgParams q = c->P;
-    q.nplan = q.ngates;
-    q.plan_pe = q.th2cap;
-    const int b = ocg::lds_layout(q, NT).bytes;
-    if (size_t(b) <= limit) {
+    q.nplan = q.ngates + ocg_host::step_gauge_moves(q);
+    q.plan_pe = 0;
+    const int b0 = ocg::lds_layout(q, NT).bytes;
+    q.plan_pe = 64;
+    const int per = (ocg::lds_layout(q, NT).bytes - b0 + 63) / 64;  // bytes per element, all slots
+    const int want = std::max(q.th2cap, q.max_site_cap);
+    q.plan_pe = std::min(want, per > 0 ? int((long(limit) - b0) / per) - 8 : 0);
+    while (q.plan_pe >= 32 && size_t(ocg::lds_layout(q, NT).bytes) > limit) q.plan_pe -= 8;
+    if (q.plan_pe >= 32) {
       c->P.nplan = q.nplan;
       c->P.plan_pe = q.plan_pe;
-      c->P.lds_bytes = b;
+      c->P.lds_bytes = ocg::lds_layout(q, NT).bytes;
     }
   }
   if (size_t(l.bytes) > limit)

@@ -80,6 +80,23 @@ inline void gate_tables(OcgParams& P, double J, std::vector<double>& gf, std::ve
   P.gtotal = off;
 }
 
+// Decompositions one step performs: one per gate plus the gauge moves of
+// MPS::position between gates (the centre walk of doStep,
+// src/BH_tDMRG.cpp:173-218, as Chain::step runs it).
+inline int step_gauge_moves(const OcgParams& P) {
+  int centre = 1, moves = 0;
+  for (int g = 0; g < P.ngates; ++g) {
+    const int i1 = P.gate_i1[g], i2 = i1 + 1;
+    const bool more = g + 1 < P.ngates;
+    const int ni1 = more ? P.gate_i1[g + 1] : 0, ni2 = ni1 + 1;
+    const bool fromleft = more && ni1 >= i2;
+    centre = fromleft ? i2 : i1;
+    const int target = !more ? 1 : (fromleft ? ni1 : ni2);
+    moves += centre > target ? centre - target : target - centre;
+  }
+  return moves;
+}
+
 // Fills everything in P except lds_bytes and the gate tables.  md receives
 // the per-sector rank bound min(Maxm, HS_left(b,q), HS_right(L-b,Q-q)).
 // Returns an empty string on success, else the error.
