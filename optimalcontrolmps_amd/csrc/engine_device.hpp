@@ -1288,44 +1288,86 @@ struct Chain {
           const double g = zc(Gc[GOFF[q] + i * n + i]).x;
           lam = g > 0 ? g : 0.0;
           LAM[e] = lam;
-          EQ[e] = q;
         }
-        wsync();
-        // global rank (descending; ties by flat index) and rank within the block
-        int rk = 0, jb = 0;
-        if (act) {
-          int f = 0;
-          for (; f + 3 < T; f += 4) {
-            const double l0 = LAM[f], l1 = LAM[f + 1], l2 = LAM[f + 2], l3 = LAM[f + 3];
-            const int b0 = EQ[f], b1 = EQ[f + 1], b2 = EQ[f + 2], b3 = EQ[f + 3];
-            const int c0 = (l0 > lam) || (l0 == lam && f < e), c1 = (l1 > lam) || (l1 == lam && f + 1 < e);
-            const int c2_ = (l2 > lam) || (l2 == lam && f + 2 < e), c3 = (l3 > lam) || (l3 == lam && f + 3 < e);
-            rk += c0 + c1 + c2_ + c3;
-            jb += (c0 & (b0 == q)) + (c1 & (b1 == q)) + (c2_ & (b2 == q)) + (c3 & (b3 == q));
+        // Truncation (ITensor truncate; relative cutoff; floor 1e-30): in the
+        // spectrum sorted descending (ties by flat index), position j >= 1 is
+        // discarded iff j >= maxm, or the weight from j to the end is below
+        // cutoff * total, or PP[j] <= 1e-30 total; the discarded set is a
+        // suffix.  kept: not discarded and within the sector's rank bound,
+        // ordered inside its block by descending weight (rank jb).
+        bool kept = false;
+        int m;
+        double total;
+        if (T <= maxm) {
+          // maxm cannot bind: only eigenvalues below max(cut, floor) can be
+          // discarded, and every other one ranks ahead of them, so the
+          // suffix weights and ranks need the small ones alone (usually none)
+          total = wsum(lam);
+          const double cut = cutoff * total, floor_ = 1e-30 * total, thr = fmax(cut, floor_);
+          int jb = 0;
+          {
+            const int eo = act ? EOFF[q] : 0, nq = act ? NQ[q] : 0;
+            const int maxn = ISCAL[I_MAXROUNDS] + 2;  // >= every block order
+            for (int t = 0; t < maxn; ++t) {
+              const int f = eo + t;
+              const double lf = bperm(lam, (f & 63) << 2);
+              jb += (t < nq && f != e && (lf > lam || (lf == lam && f < e))) ? 1 : 0;
+            }
           }
-          for (; f < T; ++f) {
-            const double lf = LAM[f];
-            const int c = (lf > lam) || (lf == lam && f < e);
-            rk += c;
-            jb += c & (EQ[f] == q);
+          const bool small = act && (lam < thr || lam <= floor_);
+          unsigned long long M = __ballot(small);
+          bool disc = false;
+          if (M) {
+            const int nbig = T - __popcll(M);
+            double S = lam;
+            int rs = 0;
+            while (M) {
+              const int f = __ffsll((long long)M) - 1;
+              M &= M - 1;
+              const double lf = rdlane(lam, f);
+              rs += (lf > lam || (lf == lam && f < e)) ? 1 : 0;
+              if (f != e && (lf < lam || (lf == lam && f > e))) S += lf;
+            }
+            disc = small && nbig + rs >= 1 && (S < cut || lam <= floor_);
           }
-          PP[rk] = lam;
+          m = T - __popcll(__ballot(disc));
+          kept = act && !disc && jb < bound[q];
+          if (kept) KIDX[EOFF[q] + jb] = e - EOFF[q];
+        } else {
+          if (act) EQ[e] = q;
+          wsync();
+          // global rank (descending; ties by flat index) and rank within the block
+          int rk = 0, jb = 0;
+          if (act) {
+            int f = 0;
+            for (; f + 3 < T; f += 4) {
+              const double l0 = LAM[f], l1 = LAM[f + 1], l2 = LAM[f + 2], l3 = LAM[f + 3];
+              const int b0 = EQ[f], b1 = EQ[f + 1], b2 = EQ[f + 2], b3 = EQ[f + 3];
+              const int c0 = (l0 > lam) || (l0 == lam && f < e), c1 = (l1 > lam) || (l1 == lam && f + 1 < e);
+              const int c2_ = (l2 > lam) || (l2 == lam && f + 2 < e), c3 = (l3 > lam) || (l3 == lam && f + 3 < e);
+              rk += c0 + c1 + c2_ + c3;
+              jb += (c0 & (b0 == q)) + (c1 & (b1 == q)) + (c2_ & (b2 == q)) + (c3 & (b3 == q));
+            }
+            for (; f < T; ++f) {
+              const double lf = LAM[f];
+              const int c = (lf > lam) || (lf == lam && f < e);
+              rk += c;
+              jb += c & (EQ[f] == q);
+            }
+            PP[rk] = lam;
+          }
+          wsync();
+          total = wsum(act ? PP[lane] : 0.0);
+          const double cut = cutoff * total, floor_ = 1e-30 * total;
+          const int j = T - 1 - lane;  // lane 0 = smallest
+          const double v = j >= 0 ? PP[j] : 0.0;
+          const double suf = wscan(v);
+          const bool disc = j >= 1 && (j >= maxm || suf < cut || v <= floor_);
+          m = T - __popcll(__ballot(disc));
+          kept = act && rk < m && jb < bound[q];
+          if (kept) KIDX[EOFF[q] + jb] = e - EOFF[q];
         }
-        wsync();
         pf(18);
-        // truncation (ITensor truncate; relative cutoff; floor 1e-30): the
-        // discarded set {j >= 1 : j >= maxm or sum_{i>=j} PP[i] < cutoff*total
-        // or PP[j] <= 1e-30 total} is a suffix of the sorted spectrum
-        const double total = wsum(act ? PP[lane] : 0.0);
-        const double cut = cutoff * total, floor_ = 1e-30 * total;
-        const int j = T - 1 - lane;  // lane 0 = smallest
-        const double v = j >= 0 ? PP[j] : 0.0;
-        const double suf = wscan(v);
-        const bool disc = j >= 1 && (j >= maxm || suf < cut || v <= floor_);
-        const int m = T - __popcll(__ballot(disc));
-        // kept vectors: global rank < m and within the sector's rank bound
-        const bool kept = act && rk < m && jb < bound[q];
-        if (kept) KIDX[EOFF[q] + jb] = e - EOFF[q];
         const double kw = wsum(kept ? lam : 0.0);
         int kq = 0;
         for (int s = 0; s < Q1; ++s) {

@@ -32,3 +32,11 @@ for k in range(8):
 tm, pm, rm = np.median(tr), np.median(pl), np.median(ro)
 print(f"trajectory {tm:.3f} ms ({1e3 * tm / 200:.1f} us/step)  pipeline {pm:.3f} ms  row_overlaps {rm:.3f} ms  "
       f"pipeline/trajectory {pm / tm:.3f}")
+# critical-path probe: the pipeline with row subsets (row 1 is the longest)
+for rows in ([1], list(range(1, 200, 8)), list(range(1, 200, 2)), list(range(1, 200))):
+    ts = []
+    for k in range(5):
+        eng.reset_stats()
+        eng.hessian(u, rows)
+        ts.append(eng.stats(5)["ms"])
+    print(f"pipeline with {len(rows):3d} rows: {np.median(ts):.3f} ms")
