@@ -1026,38 +1026,69 @@ struct Chain {
   }
   __device__ __forceinline__ static zc bpermz(zc v, int addr) { return c2(bperm(v.x, addr), bperm(v.y, addr)); }
   template <int S>
-  __device__ OCG_INLINE void jacobi_reg(lzp Gc, lzp Wc, int maxr) {
+  __device__ OCG_INLINE void jacobi_reg(lzp Gc, lzp Wc, int maxr, const LDS int* gd) {
     constexpr int GS = S * S;     // lanes per block
     constexpr int BPW = 64 / GS;  // blocks per wave
+    constexpr int MR = S - 1;     // rounds per sweep, at most
     const int Q1 = P.Q1;
     const int i = (lane / S) % S, j = lane % S, rb = lane & ~(GS - 1);
     const int wave = tid >> 6;
     auto at = [&](int r, int c) { return (rb + r * S + c) << 2; };  // bpermute byte address of (r, c)
+    const int aii = at(i, i), ajj = at(j, j);
     for (int b0 = wave * BPW; b0 < Q1; b0 += BPW * NW) {
       const int q = b0 + lane / GS;
       const bool blk_ok = q < Q1;
       const int n = blk_ok ? NQ[q] : 0, m = blk_ok ? MQ[q] : 0, go = blk_ok ? GOFF[q] : 0;
       const bool valid = i < n && j < n;
       const int loc = go + i * n + j;
-      zc g = valid ? zc(Gc[loc]) : c2(0.0, 0.0);
-      zc w = valid ? zc(Wc[loc]) : c2(i == j ? 1.0 : 0.0, 0.0);
-      // partners of i and j in every round (3 bits each; idle / padded: self)
-      int pti = 0, ptj = 0;
-      for (int rnd = 0; rnd < maxr; ++rnd) {
+      zc g = c2(0.0, 0.0), w;
+      if (gd) {
+        // Gram element straight from the plan's descriptor (no Gram phase):
+        // the same sums, in the same order, as the Gram phase computes
+        w = c2(i == j ? 1.0 : 0.0, 0.0);
+        if (valid) {
+          const unsigned a0 = gd[2 * loc], a1 = gd[2 * loc + 1];
+          const int st = a1 & 0xfff, len = (a1 >> 12) & 0xfff;
+          lzp Ta = TH + int(a0 & 0xffff), Tb = TH + int(a0 >> 16);
+          if (((a1 >> 24) & 1) == 0) {
+            for (int c = 0; c < len; ++c) cacc(g, Ta[c * st], cconj(Tb[c * st]));
+          } else {
+            for (int r = 0; r < len; ++r) cjacc(g, Ta[r * st], Tb[r * st]);
+          }
+        }
+      } else {
+        g = valid ? zc(Gc[loc]) : c2(0.0, 0.0);
+        w = valid ? zc(Wc[loc]) : c2(i == j ? 1.0 : 0.0, 0.0);
+      }
+      // per-round roles: partners of i and j (idle / padded: self), the
+      // bpermute addresses of the two rotations and three partner elements
+      int arow[MR], acol[MR], aipj[MR], apij[MR], apipj[MR], fl[MR];
+#pragma unroll
+      for (int rnd = 0; rnd < MR; ++rnd) {
         int pi = i, pj = j, t;
-        if (i < n && jpair(i, rnd, m, n, t) >= 0) pi = t;
-        if (j < n && jpair(j, rnd, m, n, t) >= 0) pj = t;
-        pti |= pi << (3 * rnd);
-        ptj |= pj << (3 * rnd);
+        if (rnd < maxr) {
+          if (i < n && jpair(i, rnd, m, n, t) >= 0) pi = t;
+          if (j < n && jpair(j, rnd, m, n, t) >= 0) pj = t;
+        }
+        arow[rnd] = at(i < pi ? i : pi, i < pi ? pi : i);
+        acol[rnd] = at(j < pj ? j : pj, j < pj ? pj : j);
+        aipj[rnd] = at(i, pj);
+        apij[rnd] = at(pi, j);
+        apipj[rnd] = at(pi, pj);
+        // bit 0 pivot (i < j paired), 1 j < pj, 2 i < pi, 3 j moves, 4 i moves, 5 pi == j
+        fl[rnd] = (i < j && pi == j ? 1 : 0) | (j < pj ? 2 : 0) | (i < pi ? 4 : 0) | (pj != j ? 8 : 0) |
+                  (pi != i ? 16 : 0) | (pi == j ? 32 : 0);
       }
       int sweep = 0;
       bool done = false;
       for (; sweep < 40; ++sweep) {
         bool flag = false;
-        for (int rnd = 0; rnd < maxr; ++rnd) {
-          const int pi = (pti >> (3 * rnd)) & 7, pj = (ptj >> (3 * rnd)) & 7;
+#pragma unroll
+        for (int rnd = 0; rnd < MR; ++rnd) {
+          if (rnd >= maxr) break;
+          const int f = fl[rnd];
           // pivot lanes: rotation of pair (i, j)
-          const double dpp = bperm(g.x, at(i, i)), dqq = bperm(g.x, at(j, j));
+          const double dpp = bperm(g.x, aii), dqq = bperm(g.x, ajj);
           // early exit: no pair of the wave's blocks passes the rotation
           // predicate, so the rest of this sweep is a chain of exact no-ops
           // and the end-of-sweep test would stop after it (same result)
@@ -1068,19 +1099,19 @@ struct Chain {
           zc cs, e;
           double sh;
           jrot_fast(g, dpp, dqq, cs, e, sh);
-          const bool piv = i < j && pi == j;
+          const bool piv = f & 1;
           cs = piv ? cs : c2(1.0, 0.0);
           sh = piv ? sh : 0.0;
           // rotations of the column pair (j, pj) and the row pair (i, pi)
-          const int aj = at(j < pj ? j : pj, j < pj ? pj : j), ai = at(i < pi ? i : pi, i < pi ? pi : i);
-          const zc csj = bpermz(cs, aj), ej = bpermz(e, aj), csi = bpermz(cs, ai), ei = bpermz(e, ai);
-          const double shj = bperm(sh, aj);
-          const zc g01 = bpermz(g, at(i, pj)), g10 = bpermz(g, at(pi, j)), g11 = bpermz(g, at(pi, pj));
-          const zc w1 = bpermz(w, at(i, pj));
-          const bool rotj = pj != j && csj.y != 0.0, roti = pi != i && csi.y != 0.0;
+          const zc csj = bpermz(cs, acol[rnd]), ej = bpermz(e, acol[rnd]);
+          const zc csi = bpermz(cs, arow[rnd]), ei = bpermz(e, arow[rnd]);
+          const double shj = bperm(sh, acol[rnd]);
+          const zc g01 = bpermz(g, aipj[rnd]), g10 = bpermz(g, apij[rnd]), g11 = bpermz(g, apipj[rnd]);
+          const zc w1 = bpermz(w, aipj[rnd]);
+          const bool rotj = (f & 8) && csj.y != 0.0, roti = (f & 16) && csi.y != 0.0;
           zc jjj, jpj, jii, jpi;
-          jcol(j < pj, csj, ej, jjj, jpj);
-          jcol(i < pi, csi, ei, jii, jpi);
+          jcol(f & 2, csj, ej, jjj, jpj);
+          jcol(f & 4, csi, ei, jii, jpi);
           jjj = rotj ? jjj : c2(1, 0);
           jpj = rotj ? jpj : c2(0, 0);
           jii = roti ? jii : c2(1, 0);
@@ -1093,10 +1124,10 @@ struct Chain {
           cacc(r1, g11, jpj);
           zc out = cjmul(jii, r0);
           cjacc(out, jpi, r1);
-          const bool zero = rotj && roti && pi == j;
+          const bool zero = rotj && roti && (f & 32);
           const bool diag = rotj && i == j;
           out = zero ? c2(0, 0) : out;
-          out = diag ? c2(g.x + (j < pj ? -shj : shj), 0) : out;
+          out = diag ? c2(g.x + ((f & 2) ? -shj : shj), 0) : out;
           if (rnd == maxr - 1)  // convergence: the rotation predicate on the sweep's output
             flag = valid && i < j && jneed(cabs2(out), dpp, dqq);
           g = out;
@@ -1114,26 +1145,26 @@ struct Chain {
     }
   }
 
-  __device__ OCG_INLINE void jacobi(lzp& Gc, lzp& Wc) {
+  // gd: Gram descriptors of a plan hit (the register path forms the Gram
+  // elements itself; only for 1 <= maxr <= 7)
+  __device__ OCG_INLINE void jacobi(lzp& Gc, lzp& Wc, const LDS int* gd = nullptr) {
     constexpr int JB_IT = 4, JA_IT = 2;
     lzp Gn = (Gc == G) ? G2 : G;
     lzp Wn = (Wc == W) ? W2 : W;
     const int maxr = ISCAL[I_MAXROUNDS];
     if (maxr <= 0) return;
-#ifndef OCG_NO_REG_JACOBI
     if (maxr <= 3) {  // every block of order <= 4
       pf(13);
-      jacobi_reg<4>(Gc, Wc, maxr);
+      jacobi_reg<4>(Gc, Wc, maxr, gd);
       sync();
       return;
     }
     if (maxr <= 7) {  // every block of order <= 8
       pf(13);
-      jacobi_reg<8>(Gc, Wc, maxr);
+      jacobi_reg<8>(Gc, Wc, maxr, gd);
       sync();
       return;
     }
-#endif
     const int npair = POFF[P.Q1];
     const int nel = GOFF[P.Q1];
     JD dB[JB_IT];
@@ -1223,8 +1254,11 @@ struct Chain {
     }
     sync();
     pf(2);
-    // Gram matrices and identity eigenvectors
-    if (phit) {
+    // Gram matrices and identity eigenvectors (on a plan hit with blocks of
+    // order 2..8 the register Jacobi forms them itself)
+    const bool fuse = phit && ps[2] >= 1 && ps[2] <= 7;
+    if (fuse) {
+    } else if (phit) {
       const int nel = GOFF[Q1];
       const LDS int* gdp = ps + pl.GD;
       for (int e = tid; e < nel; e += NT) {
@@ -1267,11 +1301,11 @@ struct Chain {
         }
       }
     }
-    sync();
+    if (!fuse) sync();
     lzp Gc = G;
     lzp Wc = W;
     pf(3);
-    jacobi(Gc, Wc);
+    jacobi(Gc, Wc, fuse ? ps + pl.GD : nullptr);
     pf(4);
     // eigenvalues (clamped at 0) and their blocks
     const int T = EOFF[Q1];
