@@ -667,9 +667,12 @@ struct Chain {
   }
 
   // pre-phase -> hopping gate (per Δ = n1+n2 block) -> post-phase, on every
-  // (a, c) vector of Θ.  mode 0: left-moving (UF both, optional lonely UT on
-  // n2); mode 1: right-moving (UT both after the gate).  One thread per
-  // output element; the result goes to X and the TH/X buffers are swapped.
+  // (a, c) vector of Θ.  mode 0: left-moving (UF both, lonely & 1: the lonely
+  // UT on n2 of an even chain); mode 1: right-moving (UT both after the gate;
+  // lonely & 2: the lonely U_from of site L of an odd chain, doStep
+  // src/BH_tDMRG.cpp:133-136, applied to the gate's input instead of the site,
+  // since site L is untouched until this gate).  One thread per output
+  // element; the result goes to X and the TH/X buffers are swapped.
   __device__ OCG_INLINE void apply_gate(int i1, int forward, int mode, int lonely) {
     pf(1);
     const int p = P.p;
@@ -689,10 +692,11 @@ struct Chain {
           const int n1 = lo + x, n2 = D - n1;
           zc z = TH[(unsigned(gd[1 + (x >> 1)]) >> (16 * (x & 1))) & 0xffff];
           if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
+          else if (lonely & 2) z = cmul(z, UF[n2]);
           cacc(acc, g[x], z);
         }
         if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
-        else if (lonely) acc = cmul(acc, UT[a2]);
+        else if (lonely & 1) acc = cmul(acc, UT[a2]);
         X[e] = acc;
       }
       sync();
@@ -724,6 +728,7 @@ struct Chain {
           const int ad = THO[qs] + (ro + ia) * THC[qs] + co + ic;
           zc z = TH[ad];
           if (mode == 0) z = cmul(z, cmul(UF[n1], UF[n2]));
+          else if (lonely & 2) z = cmul(z, UF[n2]);
           cacc(acc, g[x], z);
           if (rr) {
             pk |= ad << (16 * (x & 1));
@@ -731,7 +736,7 @@ struct Chain {
           }
         }
         if (mode == 1) acc = cmul(acc, cmul(UT[a1], UT[a2]));
-        else if (lonely) acc = cmul(acc, UT[a2]);
+        else if (lonely & 1) acc = cmul(acc, UT[a2]);
         X[e] = acc;
       }
     }
@@ -1549,8 +1554,13 @@ struct Chain {
     const int xt = XOFF[Q1], yt = YOFF[Q1];
     const int pm = ISCAL[I_P2];  // 1: factor plan, 2: record it
     if (pm == 1) {
-      // X: exact side u = W[a + w], else Θ w (len terms, Θ stride st, W stride n)
-      for (int e = tid; e < xt; e += NT) {
+      // X: exact side u = W[a + w], else Θ w (len terms, Θ stride st, W stride n).
+      // With two or more waves, X goes to wave 0 and Y to wave 1 (the two
+      // factors are independent), else one after the other.
+      const int wv = tid >> 6;
+      const int xs = NW >= 2 ? (wv == 0 ? lane : xt) : tid, xstep = NW >= 2 ? 64 : NT;
+      const int ys = NW >= 2 ? (wv == 1 ? lane : yt) : tid, ystep = NW >= 2 ? 64 : NT;
+      for (int e = xs; e < xt; e += xstep) {
         const i4 dd = *(const LDS i4*)(ps + pl.XD + 4 * e);
         const int a = dd[0] & 0xffff, g = unsigned(dd[0]) >> 16, dest = dd[1] & 0xffff, len = unsigned(dd[1]) >> 16;
         const int eb = dd[2] & 0xffff, j = unsigned(dd[2]) >> 16, n = dd[3] & 0xfff, st = (dd[3] >> 12) & 0x7ffff;
@@ -1573,7 +1583,7 @@ struct Chain {
       }
       pf(23);
       // Y: exact side v^H = conj(W[a + w]), else w^H Θ
-      for (int e = tid; e < yt; e += NT) {
+      for (int e = ys; e < yt; e += ystep) {
         const i4 dd = *(const LDS i4*)(ps + pl.YD + 4 * e);
         const int a = dd[0] & 0xffff, g = unsigned(dd[0]) >> 16, dest = dd[1] & 0xffff, len = unsigned(dd[1]) >> 16;
         const int eb = dd[2] & 0xffff, j = unsigned(dd[2]) >> 16, n = dd[3] & 0xfff, st = (dd[3] >> 12) & 0x7ffff;
@@ -1964,14 +1974,15 @@ struct Chain {
       PH[p + tid] = c2(cos(at), sin(at));
     }
     sync();
-    if (L % 2 != 0) site_phase(L, PH);  // lonely U_from on site L (:133-136)
+    // the lonely U_from on site L of an odd chain (:133-136) is applied by the
+    // gate (L-1, L) (apply_gate lonely & 2)
     int centre = 1, gslot = 0;
     bool movingFromLeft = true;
     for (int g = 0; g < P.ngates; ++g) {
       const int i1 = P.gate_i1[g], i2 = i1 + 1;
       build_theta(i1, g);
       if (movingFromLeft) apply_gate(i1, forward, 0, (i2 == L && L % 2 == 0) ? 1 : 0);
-      else apply_gate(i1, forward, 1, 0);
+      else apply_gate(i1, forward, 1, (L % 2 != 0 && i2 == L) ? 2 : 0);
       // next gate: right of this one -> Fromleft, centre i2, move to ni1;
       //            left of it / last -> Fromright, centre i1, move to ni2 / 1
       const bool more = g + 1 < P.ngates;
