@@ -12,6 +12,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -347,7 +348,9 @@ static int finish_params(ocg_ctx* c) {
   // the gauge moves between them) when their 16-bit offsets suffice; the
   // per-slot element capacity is the two-site / site bound, shrunk to the LDS
   // left over (a decomposition larger than its slot just runs unplanned)
-  if (c->P.cap < 65536 && c->P.thcap < 65536 && c->P.evcap < 4096) {
+  const char* np = std::getenv("OCG_NO_PLANS");  // diagnostic / test switch: general path only
+  const bool plans_off = np && np[0] && np[0] != '0';
+  if (!plans_off && c->P.cap < 65536 && c->P.thcap < 65536 && c->P.evcap < 4096) {
     OcgParams q = c->P;
     q.nplan = q.ngates + ocg_host::step_gauge_moves(q);
     q.plan_pe = 0;

@@ -199,3 +199,53 @@ def test_fused_equals_unfused_bitwise(states):
     rows = list(range(1, len(u) - 1))
     parts = [eng.hessian(u, rows[k::4])[0] for k in range(4)]
     assert np.array_equal(sum(parts), H2)
+
+
+def _with_plans(flag, fn):
+    import os
+    old = os.environ.get("OCG_NO_PLANS")
+    os.environ["OCG_NO_PLANS"] = "0" if flag else "1"
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ["OCG_NO_PLANS"]
+        else:
+            os.environ["OCG_NO_PLANS"] = old
+
+
+@pytest.mark.parametrize("L,p,N,J,Ui,Uf,cut", [(5, 5, 5, 1.0, 2.5, 50.0, 1e-8), (5, 6, 5, 1.0, 2.0, 12.0, 1e-4),
+                                               (4, 3, 4, 1.0, 2.0, 10.0, 1e-3)])
+def test_plans_bitwise_neutral(states, L, p, N, J, Ui, Uf, cut):
+    """decomposition plans cache index arithmetic only: the fused getHessian with
+    plans on equals the general path bitwise, also when truncation changes the
+    bond dimensions from step to step (cutoff 1e-4 / 1e-3: plan misses and
+    re-recordings)"""
+    u = np.random.default_rng(23).uniform(2, 10, 41)
+    tgt, ini = st_of(states, L, p, N, J, Uf), st_of(states, L, p, N, J, Ui)
+
+    def run():
+        eng = engine(L, p, N, J, 0.01, cut, 80)
+        eng.set_states(tgt, ini)
+        H, divT, F = eng.hessian(u)
+        return H, divT, F, eng.info.lds_bytes
+
+    H1, d1, F1, lds1 = _with_plans(True, run)
+    H0, d0, F0, lds0 = _with_plans(False, run)
+    assert lds1 > lds0  # the plan slots are really there
+    assert np.array_equal(H1, H0) and np.array_equal(d1, d0) and F1 == F0
+
+
+def test_truncation_heavy_vs_oracle(states):
+    """cutoff 1e-4: bond dimensions shrink and grow along the trajectories (plan
+    misses); Hessian and gradient against the live oracle"""
+    L, p, N, J, cut = 5, 6, 5, 1.0, 1e-4
+    u = np.random.default_rng(31).uniform(2, 10, 15)
+    tgt, ini = st_of(states, L, p, N, J, 12.0), st_of(states, L, p, N, J, 2.0)
+    eng = engine(L, p, N, J, 0.01, cut)
+    eng.set_states(tgt, ini)
+    H, divT, F = eng.hessian(u)
+    oc = O.OC(O.Stepper(L, p, N, J, 0.01, cut), as_orc(tgt), as_orc(ini), len(u), 0.0)
+    Ho = oc.hessian(u, 4)
+    assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+    assert np.abs(0.01 * (divT * F * 1j).real - oc.gradient(u)).max() < 1e-6
