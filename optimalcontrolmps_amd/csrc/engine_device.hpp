@@ -309,6 +309,8 @@ struct Chain {
   LDS int *NQ0, *SIDE0, *MQ0, *GOFF0, *EOFF0, *POFF0, *XOFF0, *YOFF0;
   PlanLayout pl;
   bool phit = false;  // the current slot's key matched (uniform)
+  double ph_u = __builtin_nan("");  // control value of PH[p..2p) (NaN: none yet)
+  int ph_dir = -1;
   unsigned long long pf_last = 0;
   int pf_cur = 0;
   // algorithmic-traffic model accumulators (per lane, summed at the end)
@@ -863,16 +865,17 @@ struct Chain {
     y = fma(y, fma(-x, y, 1.0), y);
     return fma(y, fma(-x, y, 1.0), y);
   }
-  __device__ __forceinline__ static void jrot_fast(zc bv, double app, double aqq, zc& cs, zc& e, double& shift) {
-    double r2 = bv.x * bv.x + bv.y * bv.y;
-    const bool need = jneed(r2, app, aqq);
-    double sc = 1.0;
+  // need = jneed(|bv|^2, app, aqq), evaluated by the caller.  Branch-free:
+  // the power-of-two rescale factor is 1 (exact) unless a rescale is needed.
+  __device__ __forceinline__ static void jrot_fast(zc bv, double app, double aqq, bool need, zc& cs, zc& e,
+                                                   double& shift) {
     const double mb = fmax(fabs(bv.x), fabs(bv.y)), sz = fabs(app) + fabs(aqq);
-    if (need && (mb < 1e-120 || mb > 1e120 || sz > 1e120)) {
-      sc = ldexp(1.0, -ilogb(fmax(mb, sz)));
-      bv = cscale(bv, sc); app *= sc; aqq *= sc;
-      r2 = bv.x * bv.x + bv.y * bv.y;
-    }
+    const bool resc = need && (mb < 1e-120 || mb > 1e120 || sz > 1e120);
+    const double sc = resc ? ldexp(1.0, -ilogb(fmax(mb, sz))) : 1.0;
+    bv = cscale(bv, sc);
+    app *= sc;
+    aqq *= sc;
+    const double r2 = need ? bv.x * bv.x + bv.y * bv.y : 1.0;
     const double rinv = rsq_ref(r2), r = r2 * rinv;
     const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
     const double x = fma(D, D, 4.0 * r2);
@@ -1097,13 +1100,14 @@ struct Chain {
           // early exit: no pair of the wave's blocks passes the rotation
           // predicate, so the rest of this sweep is a chain of exact no-ops
           // and the end-of-sweep test would stop after it (same result)
-          if (__ballot(valid && i < j && jneed(cabs2(g), dpp, dqq)) == 0) {
+          const bool need = jneed(cabs2(g), dpp, dqq);
+          if (__ballot(valid && i < j && need) == 0) {
             done = true;
             break;
           }
           zc cs, e;
           double sh;
-          jrot_fast(g, dpp, dqq, cs, e, sh);
+          jrot_fast(g, dpp, dqq, need, cs, e, sh);
           const bool piv = f & 1;
           cs = piv ? cs : c2(1.0, 0.0);
           sh = piv ? sh : 0.0;
@@ -1967,13 +1971,26 @@ struct Chain {
     const int L = P.L, p = P.p;
     const double tau = forward ? P.dt : -P.dt;
     pf(29);
+    // U phases exp(-i u tau n(n-1) / 4) (initUGates, :74-108).  Consecutive
+    // steps of a chain share a control value (this step's u_from is the last
+    // step's u_to, same direction), so only the new set is evaluated.  The
+    // first reader is apply_gate, behind build_theta's barrier.
     if (tid < p) {
-      double nn = double(tid) * double(tid - 1);
-      double af = -0.25 * ufrom * tau * nn, at = -0.25 * uto * tau * nn;
-      PH[tid] = c2(cos(af), sin(af));
-      PH[p + tid] = c2(cos(at), sin(at));
+      const double nn = double(tid) * double(tid - 1);
+      double s, c;
+      zc f;
+      if (ufrom == ph_u && forward == ph_dir) {
+        f = PH[p + tid];
+      } else {
+        sincos(-0.25 * ufrom * tau * nn, &s, &c);
+        f = c2(c, s);
+      }
+      sincos(-0.25 * uto * tau * nn, &s, &c);
+      PH[tid] = f;
+      PH[p + tid] = c2(c, s);
     }
-    sync();
+    ph_u = uto;
+    ph_dir = forward;
     // the lonely U_from on site L of an odd chain (:133-136) is applied by the
     // gate (L-1, L) (apply_gate lonely & 2)
     int centre = 1, gslot = 0;
@@ -1995,9 +2012,31 @@ struct Chain {
       position(centre, target, &gslot);
       if (more && (i2 == ni1 || i1 == ni2)) movingFromLeft = false;
     }
-    site_phase(1, PH + p);  // lonely U_to on site 1 (:222-223)
-    double n2 = site_norm2(1);
-    if (n2 > 0) site_scale(1, 1.0 / sqrt(n2));  // psi.normalize() (:228)
+    // lonely U_to on site 1 (:222-223), then psi.normalize() (:228)
+    if (site_used(1) <= NT) {
+      // one pass: the phased element stays in a register for the scaling
+      // (same products, same per-thread sums as the three-pass form below)
+      pf(9);
+      const LDS int* B = boff(1);
+      const int tot = B[SEG];
+      zc z = c2(0.0, 0.0);
+      double acc = 0.0;
+      if (tid < tot) {
+        int n = 0;  // site 1: blocks (q = 0, n) in n order
+#pragma unroll
+        for (int t = 1; t < OCG_MAXP; ++t)
+          if (t < p && B[t] <= tid) n = t;
+        z = cmul(site(1)[tid], PH[p + n]);
+        acc = cabs2(z);
+      }
+      const double n2 = block_sum(acc);
+      if (tid < tot) site(1)[tid] = n2 > 0 ? cscale(z, 1.0 / sqrt(n2)) : z;
+      sync();
+    } else {
+      site_phase(1, PH + p);
+      double n2 = site_norm2(1);
+      if (n2 > 0) site_scale(1, 1.0 / sqrt(n2));
+    }
   }
 
   // ------------------------------------------------------------- overlaps
