@@ -222,6 +222,46 @@ __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   return l;
 }
 
+// Overlap-only kernels (<x|y>, <x|dH|y>): the MPS, four environments, the
+// two T products and the staged site; every other buffer aliases offset 0
+// and is never touched.  Small enough for several workgroups per CU.
+__host__ __device__ inline LdsLayout lds_layout_ovl(const OcgParams& P, int nt) {
+  LdsLayout l{};
+  const int Q1 = P.Q1, SEG1 = Q1 * P.p + 1;
+  const int Q1P = (Q1 + 1 + 7) & ~7;
+  auto al = [](int x) { return (x + 3) & ~3; };
+  int c = 0;
+  l.A = c; c += P.cap;
+  l.G = c; c += P.ecap;
+  l.G2 = c; c += P.ecap;
+  l.W = c; c += P.ecap;
+  l.W2 = c; c += P.ecap;
+  l.X = c; c += P.max_site_cap;
+  l.Y = c; c += P.max_site_cap;
+  l.S = c; c += P.max_site_cap;
+  l.ncplx = c;
+  int d = 0;
+  l.RED = d; d += nt / 64 + 1;
+  l.SCAL = d; d += 16;
+  l.PROF = d; d += 32;
+  l.ndbl = (d + 1) & ~1;
+  int i = 0;
+  l.DIMS = i; i = al(i + P.nsq);
+  l.DIMX = i; i = al(i + P.nsq);
+  l.BOFF = i; i = al(i + P.L * SEG1);
+  l.BOFFT = i; i = al(i + SEG1);
+  l.TCO = i; i = al(i + SEG1);
+  l.THC = i; i += Q1P;
+  l.THO = i; i += Q1P;
+  l.XOFF = i; i += Q1P;
+  l.YOFF = i; i += Q1P;
+  l.QST = i; i += Q1P;
+  l.ISCAL = i; i += 16;
+  l.nint = i;
+  l.bytes = l.ncplx * 16 + l.ndbl * 8 + l.nint * 4;
+  return l;
+}
+
 __host__ __device__ inline LdsLayout lds_layout(const OcgParams& P, int nt) {
   LdsLayout l;
   const int Q1 = P.Q1, SEG1 = Q1 * P.p + 1;
@@ -293,7 +333,7 @@ enum { kFromleft = 0, kFromright = 1 };
 enum { S_TOTAL = 0, S_KEPTW = 1 };
 enum { I_M = 0, I_MAXROUNDS = 1, I_FLAG = 2 /* ..4 */, I_THT = 8, I_P2 = 9 };
 
-template <int NT>
+template <int NT, bool OVL = false>
 struct Chain {
   static_assert(NT % 64 == 0 && NT <= 1024, "a chain is a whole number of wave64s");
   static constexpr int NW = NT / 64;
@@ -318,7 +358,7 @@ struct Chain {
 
   __device__ Chain(const OcgParams& P_, char* smem)
       : P(P_), tid(threadIdx.x), lane(threadIdx.x & 63), SEG(P_.Q1 * P_.p), w0(threadIdx.x < 64) {
-    LdsLayout l = lds_layout(P, NT);
+    LdsLayout l = OVL ? lds_layout_ovl(P, NT) : lds_layout(P, NT);
     lzp cb{(LDS double*)smem};
     A = cb + l.A; TH = cb + l.TH; G = cb + l.G; G2 = cb + l.G2; W = cb + l.W; W2 = cb + l.W2; X = cb + l.X;
     Y = cb + l.Y; CR = cb + l.CR; S = cb + l.S; GT = cb + l.GT; PH = cb + l.PH; ROT = cb + l.ROT;
@@ -546,6 +586,7 @@ struct Chain {
   __device__ OCG_INLINE void load_tables(const zc* gf, const zc* gb, const int* md) {
     for (int i = tid; i < 32; i += NT) PROF[i] = 0.0;
     for (int s = tid; s < P.nplan; s += NT) PLN[s * pl.stride] = 0;  // no plan is valid yet
+    if (OVL) return;  // overlaps need no gates, pair table or rank bounds
     // circle-method pairing table (see jpair)
     for (int e = tid; e < kPairTable; e += NT) {
       int m = 2;

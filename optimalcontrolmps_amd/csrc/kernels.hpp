@@ -17,8 +17,8 @@ struct StatAcc {
 __device__ double g_ocg_prof[32];
 #endif
 
-template <int T>
-__device__ inline void flush_stats(Chain<T>& c, double* stats, double bytes, double flops, double steps) {
+template <class CH>
+__device__ inline void flush_stats(CH& c, double* stats, double bytes, double flops, double steps) {
 #ifdef OCG_PROFILE
   c.pf(12);
   if (threadIdx.x == 0)
@@ -71,7 +71,7 @@ template <int NT>
 __device__ OCG_INLINE void body_overlaps(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                  Pool pool, const int* xs, const int* ys, int npairs, int with_dH,
                                                  zc* out, double* stats) {
-  Chain<NT> c(P, smem);
+  Chain<NT, true> c(P, smem);
   c.load_tables(gf, gb, md);
   int i = blockIdx.x;
   if (i >= npairs) return;
@@ -243,7 +243,7 @@ __device__ OCG_INLINE void body_row_overlaps(char* smem, OcgParams P, const zc* 
                                              Pool pool, int xih_base, const int* rows, int nrows, const int* rbase,
                                              Pool rs, const double* rnorm, const zc* divT, const zc* Fp, int N,
                                              double* H, double* stats) {
-  Chain<NT> c(P, smem);
+  Chain<NT, true> c(P, smem);
   c.load_tables(gf, gb, md);
   const int g = blockIdx.x;
   if (g >= rbase[nrows]) return;

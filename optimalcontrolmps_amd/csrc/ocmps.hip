@@ -110,7 +110,16 @@ struct KStat {
 struct ocg_ctx {
   int device = 0;
   OcgParams P{};
-  int lds_np = 0;  // LDS of the kernels that never step (no plan slots)
+  int lds_np = 0;   // LDS of the kernels that never step (no plan slots)
+  int lds_ovl = 0;  // LDS of the overlap-only kernels (compact layout)
+  // parameter block of the overlap-only kernels
+  OcgParams Po() const {
+    OcgParams q = P;
+    q.nplan = 0;
+    q.plan_pe = 0;
+    q.lds_bytes = lds_ovl;
+    return q;
+  }
   // parameter block of those kernels: plans off, smaller LDS
   OcgParams Pn() const {
     OcgParams q = P;
@@ -337,6 +346,7 @@ static int finish_params(ocg_ctx* c) {
   if (c->P.gtotal <= 0) return fail(c, OCG_ESTATE, "internal: gate tables must be built before the LDS layout");
   c->P.nplan = 0;
   c->P.plan_pe = 0;
+  c->lds_ovl = ocg::lds_layout_ovl(c->P, NT).bytes;
   ocg::LdsLayout l = ocg::lds_layout(c->P, NT);
   c->P.lds_bytes = l.bytes;
   c->lds_np = l.bytes;
@@ -529,7 +539,7 @@ static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::ve
   idx.insert(idx.end(), ys.begin(), ys.end());
   HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  const OcgParams Pn = c->Pn();
+  const OcgParams Pn = c->Po();
   hipLaunchKernelGGL(k_overlaps, dim3(n), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                      c->d_idx, c->d_idx + n, n, with_dH, c->d_c, c->d_stats + 1 * 3);
   if (int rc = end_kernel(c, 1)) return rc;
@@ -800,7 +810,7 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * N + 2)) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
     if (int rc = begin_kernel(c)) return rc;
-    const OcgParams Pn = c->Pn();
+    const OcgParams Pn = c->Po();
     hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                        c->d_idx, c->d_idx + N, N, 1, c->d_pc, c->d_stats + 1 * 3);
     hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
@@ -809,7 +819,7 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   }
   if (total > 0) {
     if (int rc = begin_kernel(c)) return rc;
-    const OcgParams Pn = c->Pn();
+    const OcgParams Pn = c->Po();
     hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb,
                        c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
                        c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
