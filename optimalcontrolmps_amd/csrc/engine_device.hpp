@@ -1088,6 +1088,7 @@ struct Chain {
       const int q = b0 + lane / GS;
       const bool blk_ok = q < Q1;
       const int n = blk_ok ? NQ[q] : 0, m = blk_ok ? MQ[q] : 0, go = blk_ok ? GOFF[q] : 0;
+      const int eo = blk_ok ? EOFF[q] : 0;
       const bool valid = i < n && j < n;
       const int loc = go + i * n + j;
       zc g = c2(0.0, 0.0), w;
@@ -1191,6 +1192,21 @@ struct Chain {
       if (valid) {
         Gc[loc] = g;
         Wc[loc] = w;
+      }
+      // for the truncation: eigenvalue (clamped at 0), its rank inside the
+      // block (descending, ties by index) and its sector, from the diagonal
+      // lanes of the block (both waves, no LDS round trip)
+      const double lam = g.x > 0 ? g.x : 0.0;
+      int jb = 0;
+#pragma unroll
+      for (int t = 0; t < S; ++t) {
+        const double lt = bperm(lam, at(t, t));
+        jb += (t < n && t != i && (lt > lam || (lt == lam && t < i))) ? 1 : 0;
+      }
+      if (valid && i == j) {
+        LAM[eo + i] = lam;
+        JB[eo + i] = jb;
+        EQ[eo + i] = q;
       }
     }
   }
@@ -1362,16 +1378,24 @@ struct Chain {
     if (T <= 64) {
       // one wave: ranking, truncation and the kept set in registers, ballot
       // counts per sector, wave-level fences instead of block barriers
+      // the register Jacobi (1 <= maxr <= 7) left LAM / JB / EQ behind
+      const int mr_ = ISCAL[I_MAXROUNDS];
+      const bool regj = mr_ >= 1 && mr_ <= 7;
       if (w0) {
         const int e = lane;
         const bool act = e < T;
-        const int q = blk(EOFF, e);
+        int q = 0;
         double lam = 0.0;
-        if (act) {
-          const int i = e - EOFF[q], n = NQ[q];
-          const double g = zc(Gc[GOFF[q] + i * n + i]).x;
-          lam = g > 0 ? g : 0.0;
-          LAM[e] = lam;
+        if (regj) {
+          if (act) { q = EQ[e]; lam = LAM[e]; }
+        } else {
+          q = blk(EOFF, e);
+          if (act) {
+            const int i = e - EOFF[q], n = NQ[q];
+            const double g = zc(Gc[GOFF[q] + i * n + i]).x;
+            lam = g > 0 ? g : 0.0;
+            LAM[e] = lam;
+          }
         }
         // Truncation (ITensor truncate; relative cutoff; floor 1e-30): in the
         // spectrum sorted descending (ties by flat index), position j >= 1 is
@@ -1389,9 +1413,11 @@ struct Chain {
           total = wsum(lam);
           const double cut = cutoff * total, floor_ = 1e-30 * total, thr = fmax(cut, floor_);
           int jb = 0;
-          {
+          if (regj) {
+            if (act) jb = JB[e];
+          } else {
             const int eo = act ? EOFF[q] : 0, nq = act ? NQ[q] : 0;
-            const int maxn = ISCAL[I_MAXROUNDS] + 2;  // >= every block order
+            const int maxn = mr_ + 2;  // >= every block order
             for (int t = 0; t < maxn; ++t) {
               const int f = eo + t;
               const double lf = bperm(lam, (f & 63) << 2);
