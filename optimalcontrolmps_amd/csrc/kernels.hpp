@@ -161,8 +161,8 @@ __device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, 
     int ok = 1;
     long spins = 0;
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++spins > (1L << 23) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __builtin_amdgcn_s_sleep(32);  // ~2k cycles between polls: a waiting row is idle, not a poller
+      if (++spins > (1L << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = 0;
         atomicOr(err, 2);
         break;
