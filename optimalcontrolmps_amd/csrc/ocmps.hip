@@ -133,6 +133,7 @@ struct ocg_ctx {
   std::string err;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};  // ocg_hessian phase marks
   // device buffers
   zc *d_gf = nullptr, *d_gb = nullptr;
   int* d_md = nullptr;
@@ -433,7 +434,9 @@ int ocg_create(int device, int L, int p, int npart, double J, double tstep, doub
   if ((rc = upload_gates(c))) return bail(rc);
   if ((rc = finish_params(c))) return bail(rc);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->evh[0]) != hipSuccess || hipEventCreate(&c->evh[1]) != hipSuccess ||
+      hipEventCreate(&c->evh[2]) != hipSuccess || hipEventCreate(&c->evh[3]) != hipSuccess) {
     c->err = "stream/event creation failed";
     return bail(OCG_EHIP);
   }
@@ -475,6 +478,8 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->d_rnorm) (void)hipFree(c->d_rnorm);
   if (c->d_idx2) (void)hipFree(c->d_idx2);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
+  for (auto& e : c->evh)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -788,7 +793,16 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
   const int* d_rows = c->d_rows;
   const int* d_rbase = c->d_rows + nrows;
-  if (int rc = begin_kernel(c)) return rc;
+  // divT_i = <xi_i|dH|psi_i> and F = <psi_{N-1}|target> pair lists
+  std::vector<int> idx(2 * N + 2);
+  for (int i = 0; i < N; ++i) { idx[i] = c->xi_base() + i; idx[N + i] = c->psi_base() + i; }
+  idx[2 * N] = c->psi_base() + N - 1;
+  idx[2 * N + 1] = c->slot_target();
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * N + 2)) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
+  // the three launches back to back, one host synchronisation at the end;
+  // the phase marks give the per-kernel times (ocg_kernel_stats kinds 5, 1, 6)
+  HIPCHK(c, hipEventRecord(c->evh[0], c->stream));
   // xiH workers: the xi chain publishes one state per step and one dH
   // application costs about one step, so a few workers keep up
   const int nxw = std::min(N, kXiHWorkers);
@@ -796,42 +810,41 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
                      c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->xih_base(),
                      c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err, nxw,
                      c->d_stats + 5 * 3);
-  if (int rc = end_kernel(c, 5)) return rc;
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->evh[1], c->stream));
+  const OcgParams Po = c->Po();
+  hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx, c->d_idx + N, N, 1, c->d_pc, c->d_stats + 1 * 3);
+  hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx + 2 * N, c->d_idx + 2 * N + 1, 1, 0, c->d_pc + N, c->d_stats + 1 * 3);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->evh[2], c->stream));
+  if (total > 0)
+    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf,
+                       c->d_gb, c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
+                       c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->evh[3], c->stream));
+  std::vector<zc> pc(N + 1);
+  std::vector<double> h(hn);
   int err = 0;
-  HIPCHK(c, hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(pc.data(), c->d_pc, sizeof(zc) * (N + 1), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int kinds[3] = {5, 1, 6};
+  for (int k = 0; k < 3; ++k) {
+    if (k == 2 && total == 0) break;
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->evh[k], c->evh[k + 1]));
+    c->kst[kinds[k]].ms += ms;
+    c->kst[kinds[k]].launches += 1;
+  }
   if (err) return fail(c, OCG_ENUM, "pipeline watchdog: a consumer timed out waiting for a trajectory state");
   c->have_psi = c->have_xi = c->have_xih = true;
-  // divT_i = <xi_i|dH|psi_i> and F = <psi_{N-1}|target> into d_pc (device-resident)
-  {
-    std::vector<int> idx(2 * N + 2);
-    for (int i = 0; i < N; ++i) { idx[i] = c->xi_base() + i; idx[N + i] = c->psi_base() + i; }
-    idx[2 * N] = c->psi_base() + N - 1;
-    idx[2 * N + 1] = c->slot_target();
-    if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * N + 2)) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
-    if (int rc = begin_kernel(c)) return rc;
-    const OcgParams Pn = c->Po();
-    hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
-                       c->d_idx, c->d_idx + N, N, 1, c->d_pc, c->d_stats + 1 * 3);
-    hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
-                       c->d_idx + 2 * N, c->d_idx + 2 * N + 1, 1, 0, c->d_pc + N, c->d_stats + 1 * 3);
-    if (int rc = end_kernel(c, 1)) return rc;
-  }
-  if (total > 0) {
-    if (int rc = begin_kernel(c)) return rc;
-    const OcgParams Pn = c->Po();
-    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb,
-                       c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
-                       c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
-    if (int rc = end_kernel(c, 6)) return rc;
-  }
-  std::vector<zc> pc(N + 1);
-  HIPCHK(c, hipMemcpy(pc.data(), c->d_pc, sizeof(zc) * (N + 1), hipMemcpyDeviceToHost));
   for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
   F[0] = pc[N].x;
   F[1] = pc[N].y;
-  std::vector<double> h(hn);
-  HIPCHK(c, hipMemcpy(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost));
   for (int r = 0; r < nrows; ++r) {
     const int i = rows[r];
     for (int j = i; j + 1 < N; ++j) {
