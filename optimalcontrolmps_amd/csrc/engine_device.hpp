@@ -2034,7 +2034,16 @@ struct Chain {
   // BH_tDMRG::step (src/BH_tDMRG.cpp:111-125) + doStep (:127-230).
   // The gate loop is written with one decompose call site and one gauge-move
   // call site so the (large) decomposition is inlined only twice.
-  __device__ OCG_INLINE void step(double ufrom, double uto, int forward) {
+  // final_gauge = false (trajectory chains except their last step, Hessian
+  // rows): the closing position(1) (:206-218) is left out and the
+  // orthogonality centre stays on the last gate's left site, which is
+  // normalised instead of site 1.  The state is the same (the move only
+  // regauges sites 1-2 and drops directions below the 1e-14 gauge cutoff),
+  // and everything that follows — the next step's first gate contracts sites
+  // 1 and 2 into one Θ; overlaps, norms; exactApplyMPO, whose zip-up sees an
+  // isometry at site 1 — is gauge invariant, so a chain saves one of its six
+  // decompositions per step.  ocg_steps keeps the closing move.
+  __device__ OCG_INLINE void step(double ufrom, double uto, int forward, bool final_gauge = true) {
     const int L = P.L, p = P.p;
     const double tau = forward ? P.dt : -P.dt;
     pf(29);
@@ -2075,12 +2084,18 @@ struct Chain {
       decompose(dir, P.cutoff, P.maxm, true, MD + i1 * P.Q1, i1);  // writes sites i1, i2
       plan_end();
       centre = (dir == kFromleft) ? i2 : i1;
-      const int target = !more ? 1 : (dir == kFromleft ? ni1 : ni2);
+      const int target = !more ? (final_gauge ? 1 : centre) : (dir == kFromleft ? ni1 : ni2);
       position(centre, target, &gslot);
       if (more && (i2 == ni1 || i1 == ni2)) movingFromLeft = false;
     }
     // lonely U_to on site 1 (:222-223), then psi.normalize() (:228)
-    if (site_used(1) <= NT) {
+    if (centre != 1) {
+      // the phase is diagonal in site 1's physical index (commutes with the
+      // gauge); the norm of the MPS is the norm of the centre site
+      site_phase(1, PH + p);
+      const double n2 = site_norm2(centre);
+      if (n2 > 0) site_scale(centre, 1.0 / sqrt(n2));
+    } else if (site_used(1) <= NT) {
       // one pass: the phased element stays in a register for the scaling
       // (same products, same per-thread sums as the three-pass form below)
       pf(9);

@@ -58,7 +58,7 @@ __device__ OCG_INLINE void body_trajectory(char* smem, OcgParams P, const zc* gf
   c.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
   for (int s = 0; s + 1 < N; ++s) {
     const int tn = fwd ? t + 1 : t - 1;
-    c.step(u[t], u[tn], fwd);
+    c.step(u[t], u[tn], fwd, s + 2 == N);  // closing gauge move on the last step only (Chain::step)
     c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
     t = tn;
   }
@@ -118,7 +118,7 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
   double bytes = 0, flops = 0;
   // j = i: diagonal entry (:259-264); j > i: step psiH once, then overlap (:266-278)
   for (int j = i; j + 1 < N; ++j) {
-    if (j > i) c.step(u[j - 1], u[j], 1);
+    if (j > i) c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
     zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
     const double used = c.mps_used();
     if (threadIdx.x == 0) {
@@ -198,7 +198,7 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     publish_flag(fl + t, epoch);
     for (int s = 0; s + 1 < N; ++s) {
       const int tn = fwd ? t + 1 : t - 1;
-      c.step(u[t], u[tn], fwd);
+      c.step(u[t], u[tn], fwd, s + 2 == N);  // closing gauge move on the last step only (Chain::step)
       c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
       publish_flag(fl + tn, epoch);
       t = tn;
@@ -227,7 +227,7 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     int k = rbase[r];
     c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
     for (int j = i + 1; j + 1 < N; ++j) {  // timeStepper.step(psiH, u[j-1], u[j]) (:269)
-      c.step(u[j - 1], u[j], 1);
+      c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
       ++k;
       c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
     }
