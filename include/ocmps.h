@@ -120,7 +120,12 @@ int ocg_hessian_rows(ocg_ctx* ctx, const double* u, int N, const int* rows, int 
  * device state as ocg_propagate(..,3) + ocg_xi_dH. */
 int ocg_hessian(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                 double* F);
-/* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host */
+/* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host.
+ * Gauge: the chains skip doStep's closing position(1) (src/BH_tDMRG.cpp:206-218)
+ * on every step but their last, so an intermediate psi_t / xi_t is the same
+ * state with its orthogonality centre on the last gate's left site (site 2 for
+ * L >= 3) instead of site 1; the final states (psi_{N-1}, xi_0) and everything
+ * ocg_steps returns are in the reference's gauge. */
 int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
 
 /* ------------------------------------------------------ instrumentation
