@@ -1179,6 +1179,9 @@ struct Chain {
           const bool diag = rotj && i == j;
           out = zero ? c2(0, 0) : out;
           out = diag ? c2(g.x + ((f & 2) ? -shj : shj), 0) : out;
+#ifdef OCG_PROFILE
+          if (tid == 0) PROF[30] += 1.0;  // rounds executed
+#endif
           if (rnd == maxr - 1)  // convergence: the rotation predicate on the sweep's output
             flag = valid && i < j && jneed(cabs2(out), dpp, dqq);
           g = out;

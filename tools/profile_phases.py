@@ -43,5 +43,6 @@ for what in ["trajectory(2 chains x 200 steps)", "div_t+xi_dH", "hessian_rows(19
         if pr[i] > 0:
             print(f"   {n:12s} {pr[i]:.3e} ({100*pr[i]/tot:5.1f}%)")
     if pr[21] > 0:
-        print(f"   jacobi calls {pr[21]:.0f}, sweeps/call {pr[20]/pr[21]:.2f}, rounds/sweep {pr[22]/pr[21]:.2f}")
+        print(f"   jacobi calls {pr[21]:.0f}, sweeps/call {pr[20]/pr[21]:.2f}, rounds/sweep {pr[22]/pr[21]:.2f}, "
+              f"rounds executed/call (wave 0 of the first block group) {pr[30]/pr[21]:.2f}")
 print("traj kernel ms:", eng.stats(0)["ms"], " rows ms:", eng.stats(3)["ms"])
