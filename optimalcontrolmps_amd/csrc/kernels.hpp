@@ -149,7 +149,7 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
 //   k_row_overlaps  one workgroup per stored psiH_i(j): overlap with xiH_j, H_ij
 // Producers and consumers live in one grid; consumers only ever wait on
 // blocks 0 and 1, which are dispatched first, so progress does not depend on
-// co-residency.  A watchdog (~2 s) aborts waits and flags err.
+// co-residency.  A watchdog (~2^24 polls, ~15 s) aborts waits and flags err.
 __device__ __forceinline__ void publish_flag(int* flag, int epoch) {
   __threadfence();
   __syncthreads();
@@ -162,7 +162,7 @@ __device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, 
     long spins = 0;
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
       __builtin_amdgcn_s_sleep(32);  // ~2k cycles between polls: a waiting row is idle, not a poller
-      if (++spins > (1L << 20) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (++spins > (1L << 24) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = 0;
         atomicOr(err, 2);
         break;
