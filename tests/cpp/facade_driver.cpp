@@ -424,9 +424,107 @@ static void scen_golden(Json& js) {
   js.vec("step_bond_dims", bd2);
 }
 
+// A stub TNLP driver: the callback sequence BH_nlp hands IPOPT
+// (src/BH_nlp.cpp:88-205) on a GROUP problem, with a damped Newton iteration
+// standing in for IPOPT (not installed): eval_f(new_x) -> getCost,
+// eval_grad_f -> getAnalyticGradient(x, false), eval_g -> getControl,
+// eval_h -> getHessian(x); then finalize_solution's tail (:225-262):
+// getControl / getFidelityForAllT of the initial and final coefficients and
+// the GROUP and GRAPE Hessians at the optimum.
+static stdvec solve_damped(rowmat H, stdvec g, double lam) {  // (H + lam I) p = -g, Gaussian elimination
+  const int n = int(g.size());
+  for (int i = 0; i < n; ++i) { H[i][i] += lam; g[i] = -g[i]; }
+  for (int k = 0; k < n; ++k) {
+    int piv = k;
+    for (int i = k + 1; i < n; ++i)
+      if (std::fabs(H[i][k]) > std::fabs(H[piv][k])) piv = i;
+    std::swap(H[k], H[piv]);
+    std::swap(g[k], g[piv]);
+    for (int i = k + 1; i < n; ++i) {
+      const double f = H[i][k] / H[k][k];
+      for (int j = k; j < n; ++j) H[i][j] -= f * H[k][j];
+      g[i] -= f * g[k];
+    }
+  }
+  stdvec x(n);
+  for (int i = n - 1; i >= 0; --i) {
+    double a = g[i];
+    for (int j = i + 1; j < n; ++j) a -= H[i][j] * x[j];
+    x[i] = a / H[i][i];
+  }
+  return x;
+}
+
+static void scen_nlp(Json& js) {
+  BoseHubbard sites(5, 4);
+  MPS ini = load_state(skey(5, 5, 5, 1.0, 2.5)), tgt = load_state(skey(5, 5, 5, 1.0, 50.0));
+  Stepper st(sites, 1.0, 0.01, Args(1e-8, 80));
+  const int N = 31, M = 4;
+  const double T = 0.3;
+  stdvec u0 = SeedGenerator::linspace(2.5, 50.0, N);
+  ControlBasis basis = ControlBasisFactory::buildChoppedSineBasis(u0, 0.01, T, M);
+  OC oc(tgt, ini, st, basis, 1e-6);
+  js.num("n_vars", oc.getM());
+  js.num("n_times", oc.getN());
+  stdvec x(M, 0.0);  // get_starting_point: zero coefficients (:75-84)
+  const stdvec x0 = x;
+  stdvec costs, gnorms;
+  bool grad_consistent = true, hess_symmetric = true;
+  for (int it = 0; it < 4; ++it) {
+    const double f = oc.getCost(x, true);                   // eval_f(new_x = true)
+    const stdvec g = oc.getAnalyticGradient(x, false);      // eval_grad_f(new_x = false)
+    const stdvec ctl = oc.getControl(x);                    // eval_g
+    const rowmat H = oc.getHessian(x);                      // eval_h
+    if (int(ctl.size()) != N) throw std::runtime_error("getControl size");
+    OC fresh(tgt, ini, st, basis, 1e-6);                    // the cached gradient equals a fresh one
+    const stdvec gf = fresh.getAnalyticGradient(x, true);
+    double gn = 0;
+    for (int i = 0; i < M; ++i) {
+      gn += g[i] * g[i];
+      if (std::fabs(g[i] - gf[i]) > 1e-12 * (1.0 + std::fabs(gf[i]))) grad_consistent = false;
+      for (int j = 0; j < M; ++j)
+        if (std::fabs(H[i][j] - H[j][i]) > 1e-12 * (1.0 + std::fabs(H[i][j]))) hess_symmetric = false;
+    }
+    costs.push_back(f);
+    gnorms.push_back(std::sqrt(gn));
+    // damped Newton step with backtracking on eval_f(new_x = true)
+    double hmax = 0;
+    for (int i = 0; i < M; ++i) hmax = std::max(hmax, std::fabs(H[i][i]));
+    stdvec p = solve_damped(H, g, 1e-3 * hmax + 1e-12);
+    double slope = 0;
+    for (int i = 0; i < M; ++i) slope += p[i] * g[i];
+    if (!(slope < 0))  // indefinite Hessian: steepest descent instead
+      for (int i = 0; i < M; ++i) p[i] = -g[i] / (hmax + 1e-12);
+    double a = 1.0;
+    stdvec xn(M);
+    for (int ls = 0; ls < 30; ++ls, a *= 0.5) {
+      for (int i = 0; i < M; ++i) xn[i] = x[i] + a * p[i];
+      if (oc.getCost(xn, true) < f) {
+        x = xn;  // accepted (else x stays)
+        break;
+      }
+    }
+  }
+  costs.push_back(oc.getCost(x, true));
+  js.vec("costs", costs);
+  js.vec("grad_norms", gnorms);
+  js.flag("grad_consistent", grad_consistent);
+  js.flag("hess_symmetric", hess_symmetric);
+  js.vec("x_final", x);
+  // finalize_solution (:225-262)
+  const stdvec uI = oc.getControl(x0), uF = oc.getControl(x);
+  js.vec("fid_initial", oc.getFidelityForAllT(x0));
+  js.vec("fid_final", oc.getFidelityForAllT(x));
+  js.mat("hess_group", oc.getHessian(x));
+  oc.setGRAPE(true);
+  js.mat("hess_grape", oc.getHessian(uF));
+  js.num("u_final_mid", uF[N / 2]);
+  js.num("u_initial_mid", uI[N / 2]);
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
-    std::fprintf(stderr, "usage: %s <basis|cost|gradient|hessian|sequencing|golden> <state-dir>\n", argv[0]);
+    std::fprintf(stderr, "usage: %s <basis|cost|gradient|hessian|sequencing|golden|nlp> <state-dir>\n", argv[0]);
     return 2;
   }
   g_dir = argv[2];
@@ -439,6 +537,7 @@ int main(int argc, char** argv) {
     else if (sc == "hessian") scen_hessian(js);
     else if (sc == "sequencing") scen_sequencing(js);
     else if (sc == "golden") scen_golden(js);
+    else if (sc == "nlp") scen_nlp(js);
     else throw std::runtime_error("unknown scenario " + sc);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "error: %s\n", e.what());

@@ -161,3 +161,19 @@ SEQ_KEYS = ["same_CGH", "same_bfgs_CGH", "same_GCH", "same_bfgs_GCH", "same_CHG"
 @pytest.mark.parametrize("key", SEQ_KEYS)
 def test_sequencing(res, key):
     assert res("sequencing")[key] is True                                    # tests/SequencingTest.cpp:81-263
+
+
+# ------------------------------------------------------------ BH_nlp call sequence
+def test_stub_tnlp_driver(res):
+    """BH_nlp's IPOPT callbacks (src/BH_nlp.cpp:88-205, finalize :225-262) on a
+    GROUP problem with a damped Newton loop in place of IPOPT: the cached
+    gradient equals a fresh one, the Hessian is symmetric, the cost decreases
+    and the final fidelity improves."""
+    r = res("nlp")
+    assert r["n_vars"] == 4 and r["n_times"] == 31
+    assert r["grad_consistent"] and r["hess_symmetric"]
+    c = A(r["costs"])
+    assert np.all(np.diff(c) <= 0) and c[-1] < c[0] - 0.05, c
+    assert r["fid_final"][-1] > r["fid_initial"][-1]
+    H = A(r["hess_grape"])
+    assert H.shape == (31, 31) and np.allclose(H, H.T, atol=1e-12)

@@ -72,3 +72,17 @@ def test_gpu_facade_matches_oracle_facade(statedir):
     assert np.abs(A(g["fid"]) - A(o["fid"])).max() < 1e-9
     assert g["psiT_bond_dims"] == o["psiT_bond_dims"]
     assert g["step_bond_dims"] == o["step_bond_dims"]
+
+
+def test_gpu_facade_stub_tnlp_matches_oracle(statedir):
+    """the BH_nlp call sequence through the GPU facade follows the same Newton
+    path as through the oracle facade (costs 1e-9, final coefficients 1e-6,
+    GROUP / GRAPE Hessians within 1e-6 max|H|)"""
+    g = fb.run("gpu", "nlp", statedir)
+    o = fb.run("oracle", "nlp", statedir)
+    assert g["grad_consistent"] and g["hess_symmetric"]
+    assert np.abs(A(g["costs"]) - A(o["costs"])).max() < 1e-9
+    assert np.abs(A(g["x_final"]) - A(o["x_final"])).max() < 1e-6
+    for k in ("hess_group", "hess_grape"):
+        Ho = A(o[k])
+        assert np.abs(A(g[k]) - Ho).max() <= 1e-6 * np.abs(Ho).max()
