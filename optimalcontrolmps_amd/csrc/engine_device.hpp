@@ -187,7 +187,7 @@ struct LdsLayout {
 // first operand, second operand, length, second stride).
 struct PlanLayout {
   int KEY, TRO, TCO, THR, THC, THO, BT, GA, GAW, NQ, SIDE, MQ, GOFF, EOFF, POFF, GD, KK, XOFF, YOFF, BO1, BO2, XD, YD,
-      SD, stride;
+      SD, PDO, PD, stride;
 };
 __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   PlanLayout l;
@@ -218,6 +218,8 @@ __host__ __device__ inline PlanLayout plan_layout(const OcgParams& P) {
   l.XD = i; i = al(i + 4 * P.plan_pe);
   l.YD = i; i = al(i + 4 * P.plan_pe);
   l.SD = i; i = al(i + 4 * P.plan_pe);
+  l.PDO = i; i += Q1P;
+  l.PD = i; i = al(i + 4 * P.plan_pe);
   l.stride = i;
   return l;
 }
@@ -1369,6 +1371,33 @@ struct Chain {
           }
         }
       }
+      // derived-factor products Θ w (cols-side blocks) / w^H Θ (rows-side
+      // blocks) for every eigenvector: offsets PDO and descriptors PD
+      // (Θ base, W base, length | side << 16, Θ stride | W stride << 16)
+      if (NW >= 2 && ps && w0) {
+        const int q = lane;
+        int sz = 0;
+        if (q < Q1 && NQ[q] > 0) sz = SIDE[q] ? THR[q] * NQ[q] : NQ[q] * THC[q];
+        const int inc = wscan(sz);
+        if (q < Q1) ps[pl.PDO + q] = inc - sz;
+        if (lane == 63) ps[pl.PDO + Q1] = inc;
+        wsync();
+        const int tot = ps[pl.PDO + Q1];
+        for (int e = lane; e < tot && e < P.plan_pe; e += 64) {
+          const int qq = blk(ps + pl.PDO, e);
+          const int n = NQ[qq], R = THR[qq], C = THC[qq], o = THO[qq], g = GOFF[qq], x = e - ps[pl.PDO + qq];
+          LDS int* dd = ps + pl.PD + 4 * e;
+          if (SIDE[qq]) {  // X[row][w] = sum_c Θ[row][c] W[c][w]
+            int w;
+            const int row = udiv(x, n, w);
+            dd[0] = o + row * C; dd[1] = g + w; dd[2] = C | (1 << 16); dd[3] = 1 | (n << 16);
+          } else {  // Y[w][col] = sum_r conj(W[r][w]) Θ[r][col]
+            int col;
+            const int w = udiv(x, C, col);
+            dd[0] = o + col; dd[1] = g + w; dd[2] = R; dd[3] = C | (n << 16);
+          }
+        }
+      }
     }
     if (!fuse) sync();
     lzp Gc = G;
@@ -1384,6 +1413,25 @@ struct Chain {
       // the register Jacobi (1 <= maxr <= 7) left LAM / JB / EQ behind
       const int mr_ = ISCAL[I_MAXROUNDS];
       const bool regj = mr_ >= 1 && mr_ <= 7;
+      if (NW >= 2 && phit && tid >= 64 && tid < 128) {
+        // wave 1, meanwhile: the derived-factor products for every eigenvector
+        // into CR (the factor phase then only selects and scales them); same
+        // sums in the same order as the factor phase's own loops
+        const int tot = ps[pl.PDO + Q1];
+        if (tot <= P.plan_pe)
+          for (int e = lane; e < tot; e += 64) {
+            const i4 dd = *(const LDS i4*)(ps + pl.PD + 4 * e);
+            const int len = dd[2] & 0xffff, ts_ = dd[3] & 0xffff, ws = unsigned(dd[3]) >> 16;
+            lzp Ta = TH + dd[0], Wg = Wc + dd[1];
+            zc acc = c2(0, 0);
+            if (dd[2] >> 16) {
+              for (int c = 0; c < len; ++c) cacc(acc, Ta[c * ts_], Wg[c * ws]);
+            } else {
+              for (int r = 0; r < len; ++r) cjacc(acc, Wg[r * ws], Ta[r * ts_]);
+            }
+            CR[e] = acc;
+          }
+      }
       if (w0) {
         const int e = lane;
         const bool act = e < T;
@@ -1645,9 +1693,14 @@ struct Chain {
           out = Wc[a + w];
           if (dir == kFromright) out = cscale(out, sig * inv);
         } else {
-          zc acc = c2(0, 0);
-          lzp Ta = TH + a, Wg = Wc + g + w;
-          for (int c = 0; c < len; ++c) cacc(acc, Ta[c * st], Wg[c * n]);
+          zc acc;
+          if (NW >= 2) {
+            acc = CR[a + w * g];  // precomputed Θ w (a: row base, g: w multiplier)
+          } else {
+            acc = c2(0, 0);
+            lzp Ta = TH + a, Wg = Wc + g + w;
+            for (int c = 0; c < len; ++c) cacc(acc, Ta[c * st], Wg[c * n]);
+          }
           if (dir == kFromleft) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
@@ -1668,9 +1721,14 @@ struct Chain {
           out = cconj(Wc[a + w]);
           if (dir == kFromleft) out = cscale(out, sig * inv);
         } else {
-          zc acc = c2(0, 0);
-          lzp Ta = TH + a, Wg = Wc + g + w;
-          for (int r = 0; r < len; ++r) cjacc(acc, Wg[r * n], Ta[r * st]);
+          zc acc;
+          if (NW >= 2) {
+            acc = CR[a + w * g];  // precomputed w^H Θ (a: column base, g: w multiplier)
+          } else {
+            acc = c2(0, 0);
+            lzp Ta = TH + a, Wg = Wc + g + w;
+            for (int r = 0; r < len; ++r) cjacc(acc, Wg[r * n], Ta[r * st]);
+          }
           if (dir == kFromright) out = (sig > 0) ? cscale(acc, 1.0 / sig) : c2(0, 0);
           else out = cscale(acc, inv);
         }
@@ -1711,7 +1769,8 @@ struct Chain {
         if (pm == 2 && e < P.plan_pe) {
           const bool ex = SIDE[q] == 0;
           LDS int* dd = ps + pl.XD + 4 * e;
-          dd[0] = (ex ? GOFF[q] + row * n : THO[q] + row * C) | (GOFF[q] << 16);
+          dd[0] = ex ? (GOFF[q] + row * n) | (GOFF[q] << 16)
+                     : (NW >= 2 ? (ps[pl.PDO + q] + row * n) | (1 << 16) : (THO[q] + row * C) | (GOFF[q] << 16));
           dd[1] = dest | (C << 16);
           dd[2] = EOFF[q] | (j << 16);
           dd[3] = n | (1 << 12) | (ex ? int(0x80000000u) : 0);
@@ -1750,7 +1809,8 @@ struct Chain {
         if (pm == 2 && e < P.plan_pe) {
           const bool ex = SIDE[q] == 1;
           LDS int* dd = ps + pl.YD + 4 * e;
-          dd[0] = (ex ? GOFF[q] + col * n : THO[q] + col) | (GOFF[q] << 16);
+          dd[0] = ex ? (GOFF[q] + col * n) | (GOFF[q] << 16)
+                     : (NW >= 2 ? (ps[pl.PDO + q] + col) | (C << 16) : (THO[q] + col) | (GOFF[q] << 16));
           dd[1] = dest | (R << 16);
           dd[2] = EOFF[q] | (j << 16);
           dd[3] = n | (C << 12) | (ex ? int(0x80000000u) : 0);
@@ -1758,7 +1818,8 @@ struct Chain {
       }
     }
     sync();
-    if (pm == 2 && tid == 0) ps[3] = (xt <= P.plan_pe && yt <= P.plan_pe) ? 1 : 0;
+    if (pm == 2 && tid == 0)
+      ps[3] = (xt <= P.plan_pe && yt <= P.plan_pe && (NW < 2 || ps[pl.PDO + Q1] <= P.plan_pe)) ? 1 : 0;
   }
 
   // single-site matricisation of site k into TH
