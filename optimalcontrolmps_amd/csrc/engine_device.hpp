@@ -583,7 +583,7 @@ struct Chain {
     sync();
   }
   // gate tables and the per-sector rank bound md[b][q] (Hilbert-space
-  // Schmidt-rank bound, capped by Maxm) used to clamp numerically-zero
+  // Schmidt-rank bound; Maxm is applied by decompose) used to clamp numerically-zero
   // directions out of every decomposition (guards the LDS capacities).
   __device__ OCG_INLINE void load_tables(const zc* gf, const zc* gb, const int* md) {
     for (int i = tid; i < 32; i += NT) PROF[i] = 0.0;

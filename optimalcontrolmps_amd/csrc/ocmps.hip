@@ -268,7 +268,7 @@ static int validate_dims(ocg_ctx* c, const int* dims) {
       if (v < 0) return fail(c, OCG_EINVAL, "negative bond dimension");
       if (v > c->md[b * P.Q1 + q])
         return fail(c, OCG_ECAP, "bond " + std::to_string(b) + " sector " + std::to_string(q) +
-                                      " exceeds its Schmidt-rank bound / Maxm");
+                                      " exceeds its Schmidt-rank bound");
     }
   return 0;
 }

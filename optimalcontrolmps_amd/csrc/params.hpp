@@ -98,7 +98,11 @@ inline int step_gauge_moves(const OcgParams& P) {
 }
 
 // Fills everything in P except lds_bytes and the gate tables.  md receives
-// the per-sector rank bound min(Maxm, HS_left(b,q), HS_right(L-b,Q-q)).
+// the per-sector rank bound min(HS_left(b,q), HS_right(L-b,Q-q)).  Maxm is
+// deliberately not folded in: it caps the TOTAL bond dimension of a gate
+// decomposition only (decompose applies it), while the initial/target
+// states may carry larger bonds and the gauge moves (ITensor position, no
+// Maxm) must keep them.
 // Returns an empty string on success, else the error.
 inline std::string build_params(OcgParams& P, std::vector<int>& mdv, int L, int p, int npart, double tstep,
                                 double cutoff, int maxm) {
@@ -120,14 +124,14 @@ inline std::string build_params(OcgParams& P, std::vector<int>& mdv, int L, int 
   for (int i = L - offset; i >= 1; i -= 2) P.gate_i1[g++] = i;
   P.ngates = g;
   const int Q1 = P.Q1;
-  // mdv[0 .. nsq)     : physical bound min(Maxm, HS_left(b,q), HS_right(L-b,Q-q))
+  // mdv[0 .. nsq)     : physical bound min(HS_left(b,q), HS_right(L-b,Q-q))
   // mdv[nsq .. 2 nsq) : bound inside the dH zip-up, whose bonds also carry the
   //                     MPO index: min(HS_left, 2 min(HS_left, HS_right))
   mdv.assign(2 * P.nsq, 0);
   for (int b = 0; b <= L; ++b)
     for (int q = 0; q < Q1; ++q) {
       long long a = hs_count(b, p, q), r = hs_count(L - b, p, P.Q - q);
-      mdv[b * Q1 + q] = int(std::min<long long>(std::min(a, r), P.maxm));
+      mdv[b * Q1 + q] = int(std::min(a, r));
       mdv[P.nsq + b * Q1 + q] = int(std::min<long long>(a, 2 * std::min(a, r)));
     }
   // capacities cover both the physical and the zip-up bond dimensions

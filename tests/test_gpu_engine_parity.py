@@ -249,3 +249,26 @@ def test_truncation_heavy_vs_oracle(states):
     Ho = oc.hessian(u, 4)
     assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
     assert np.abs(0.01 * (divT * F * 1j).real - oc.gradient(u)).max() < 1e-6
+
+
+@pytest.mark.parametrize("maxm", [3, 6])
+def test_maxm_binding_vs_oracle(states, maxm):
+    """Maxm binds (bond dimension capped below the exact 14): the general
+    ranking path of the truncation, plan misses on capped bonds; Hessian and
+    gradient against the live oracle, plans on/off bitwise equal"""
+    L, p, N, J = 5, 6, 5, 1.0
+    u = np.random.default_rng(41).uniform(2, 10, 13)
+    tgt, ini = st_of(states, L, p, N, J, 12.0), st_of(states, L, p, N, J, 2.0)
+
+    def run():
+        eng = engine(L, p, N, J, 0.01, 1e-8, maxm)
+        eng.set_states(tgt, ini)
+        return eng.hessian(u)
+
+    H, divT, F = _with_plans(True, run)
+    H0, d0, F0 = _with_plans(False, run)
+    assert np.array_equal(H, H0) and np.array_equal(divT, d0) and F == F0
+    oc = O.OC(O.Stepper(L, p, N, J, 0.01, 1e-8, maxm), as_orc(tgt), as_orc(ini), len(u), 0.0)
+    Ho = oc.hessian(u, 4)
+    assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+    assert np.abs(0.01 * (divT * F * 1j).real - oc.gradient(u)).max() < 1e-6
