@@ -245,25 +245,31 @@ __device__ OCG_INLINE void body_row_overlaps(char* smem, OcgParams P, const zc* 
                                              double* H, double* stats) {
   Chain<NT, true> c(P, smem);
   c.load_tables(gf, gb, md);
-  const int g = blockIdx.x;
-  if (g >= rbase[nrows]) return;
-  int lo = 0, hi = nrows - 1;  // row r with rbase[r] <= g < rbase[r+1]
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (rbase[mid] <= g) lo = mid;
-    else hi = mid - 1;
-  }
-  const int r = lo, i = rows[r], j = i + (g - rbase[r]);
-  c.load(SLOT_D(rs, P, g), SLOT_X(rs, P, g));
-  const zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
-  const double b = 32.0 * c.mps_used();
-  if (threadIdx.x == 0) {
-    const zc F = *Fp, di = divT[i], dj = divT[j];
-    const double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? rnorm[r] : 1.0);  // Re(F <xiH_j|psiH> normiH)
-    const double v2 = -(di.x * dj.x + di.y * dj.y);                          // -Re(divT_i conj(divT_j))
-    const double res = P.dt * P.dt * (v1 + v2);
-    H[(size_t)i * N + j] = res;
-    if (j > i) H[(size_t)j * N + i] = res;
+  // grid-stride over the (row, column) pairs: a few thousand resident
+  // workgroups each take several pairs (one pair per workgroup is bound by
+  // the dispatch rate, not by the work)
+  const int total = rbase[nrows];
+  double b = 0;
+  for (int g = blockIdx.x; g < total; g += gridDim.x) {
+    int lo = 0, hi = nrows - 1;  // row r with rbase[r] <= g < rbase[r+1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (rbase[mid] <= g) lo = mid;
+      else hi = mid - 1;
+    }
+    const int r = lo, i = rows[r], j = i + (g - rbase[r]);
+    c.load(SLOT_D(rs, P, g), SLOT_X(rs, P, g));
+    const zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
+    b += 32.0 * c.mps_used();
+    if (threadIdx.x == 0) {
+      const zc F = *Fp, di = divT[i], dj = divT[j];
+      const double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? rnorm[r] : 1.0);  // Re(F <xiH_j|psiH> normiH)
+      const double v2 = -(di.x * dj.x + di.y * dj.y);                          // -Re(divT_i conj(divT_j))
+      const double res = P.dt * P.dt * (v1 + v2);
+      H[(size_t)i * N + j] = res;
+      if (j > i) H[(size_t)j * N + i] = res;
+    }
+    c.sync();  // LDS reuse by the next pair
   }
   flush_stats(c, stats, b, 8.0 * b / 16.0 * 4.0, 0.0);
 }

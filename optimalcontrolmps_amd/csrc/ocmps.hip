@@ -86,6 +86,17 @@ __global__ __launch_bounds__(NT) void k_row_overlaps(OcgParams P, const zc* gf, 
                              stats);
 }
 
+// the same body on one wave per overlap: the contraction's barriers become
+// wave barriers and twice as many overlaps fit a CU (the pairs are small)
+__global__ __launch_bounds__(64) void k_row_overlaps_w(OcgParams P, const zc* gf, const zc* gb, const int* md,
+                                                       Pool pool, int xih_base, const int* rows, int nrows,
+                                                       const int* rbase, Pool rs, const double* rnorm,
+                                                       const zc* divT, const zc* F, int N, double* H, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_row_overlaps<64>(smem, P, gf, gb, md, pool, xih_base, rows, nrows, rbase, rs, rnorm, divT, F, N, H,
+                             stats);
+}
+
 __global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                               Pool pool, const int* slots, int n, const double* u, int u_stride,
                                               int nsteps, int forward, double* stats) {
@@ -340,6 +351,7 @@ static int set_lds(ocg_ctx* c) {
   HIPCHK(c, hipFuncSetAttribute((const void*)k_steps, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIPCHK(c, hipFuncSetAttribute((const void*)k_pipeline, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIPCHK(c, hipFuncSetAttribute((const void*)k_row_overlaps, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_row_overlaps_w, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   return 0;
 }
 
@@ -819,8 +831,21 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
                      c->d_idx + 2 * N, c->d_idx + 2 * N + 1, 1, 0, c->d_pc + N, c->d_stats + 1 * 3);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->evh[2], c->stream));
-  if (total > 0)
-    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(total)), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf,
+  static const int rov_w = [] {  // A/B switch: OCG_ROWOV_WAVE=0 -> two-wave row overlaps
+    const char* e = std::getenv("OCG_ROWOV_WAVE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  static const int rov_grid = [] {  // A/B: resident workgroups of the row overlaps (0: one per pair)
+    const char* e = std::getenv("OCG_ROWOV_GRID");
+    return e ? std::atoi(e) : 4096;
+  }();
+  const int rgrid = (rov_grid > 0 && size_t(rov_grid) < total) ? rov_grid : int(total);
+  if (total > 0 && rov_w)
+    hipLaunchKernelGGL(k_row_overlaps_w, dim3(unsigned(rgrid)), dim3(64), Po.lds_bytes, c->stream, Po, c->d_gf,
+                       c->d_gb, c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
+                       c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
+  else if (total > 0)
+    hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(rgrid)), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf,
                        c->d_gb, c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
                        c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
   HIPCHK(c, hipGetLastError());
