@@ -34,6 +34,12 @@
 #define OCG_INLINE __attribute__((always_inline))
 #endif
 
+// Jacobi rotation threshold |g_pq|^2 > OCG_JTOL2 |g_pp g_qq| (relative
+// off-diagonal 1e-14 by default)
+#ifndef OCG_JTOL2
+#define OCG_JTOL2 1e-28
+#endif
+
 namespace ocg {
 
 // ---------------------------------------------------------------- complex
@@ -864,7 +870,7 @@ struct Chain {
   // the convergence test, so a converged sweep performs no rotation.
   __device__ __forceinline__ static bool jneed(double b2, double app, double aqq) {
     const double s = fabs(app) + fabs(aqq);
-    return b2 > 1e-28 * fabs(app * aqq) + 1e-36 * s * s && b2 > 0.0;
+    return b2 > OCG_JTOL2 * fabs(app * aqq) + 1e-36 * s * s && b2 > 0.0;
   }
   // Phase A: complex Jacobi rotation zeroing g[p][q] of pair t in round rnd.
   // With D = aqq - app, b = g[p][q], r = |b| (the classical tan formula
