@@ -160,7 +160,8 @@ __device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, 
   if (threadIdx.x == 0) {
     int ok = 1;
     long spins = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+    // relaxed polls (no L2 invalidate per poll), one acquire fence on success
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
       __builtin_amdgcn_s_sleep(32);  // ~2k cycles between polls: a waiting row is idle, not a poller
       if (++spins > (1L << 24) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = 0;
@@ -168,6 +169,7 @@ __device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, 
         break;
       }
     }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // agent scope (the default)
     c.ISCAL[15] = ok;
   }
   __syncthreads();
