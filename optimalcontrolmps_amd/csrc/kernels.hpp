@@ -169,7 +169,7 @@ __device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, 
         break;
       }
     }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // agent scope (the default)
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // once per wait (system scope)
     c.ISCAL[15] = ok;
   }
   __syncthreads();
