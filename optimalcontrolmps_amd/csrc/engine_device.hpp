@@ -1082,6 +1082,27 @@ struct Chain {
     return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
   }
   __device__ __forceinline__ static zc bpermz(zc v, int addr) { return c2(bperm(v.x, addr), bperm(v.y, addr)); }
+  // DPP lane swaps inside a 16-lane row (one 4x4 block, lane 4 i + j):
+  // xcol = lane ^ k (quad_perm), xrow = lane ^ 4k (row/half mirrors
+  // composed with a quad swap), k = rnd + 1; rnd is a constant after unrolling
+  template <int CTRL>
+  __device__ __forceinline__ static double dppd(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+  }
+  template <int CTRL>
+  __device__ __forceinline__ static zc dppz(zc v) { return c2(dppd<CTRL>(v.x), dppd<CTRL>(v.y)); }
+  static constexpr int kQx1 = 0xB1, kQx2 = 0x4E, kQx3 = 0x1B, kRowMirror = 0x140, kHalfMirror = 0x141;
+  __device__ __forceinline__ static zc xcol(zc v, int rnd) {
+    return rnd == 0 ? dppz<kQx1>(v) : rnd == 1 ? dppz<kQx2>(v) : dppz<kQx3>(v);
+  }
+  __device__ __forceinline__ static zc xrow(zc v, int rnd) {
+    if (rnd == 0) return dppz<kQx3>(dppz<kHalfMirror>(v));        // ^7 ^3 = ^4
+    if (rnd == 1) return dppz<kHalfMirror>(dppz<kRowMirror>(v));  // ^15 ^7 = ^8
+    return dppz<kQx3>(dppz<kRowMirror>(v));                       // ^15 ^3 = ^12
+  }
   template <int S>
   __device__ OCG_INLINE void jacobi_reg(lzp Gc, lzp Wc, int maxr, const LDS int* gd) {
     constexpr int GS = S * S;     // lanes per block
@@ -1124,7 +1145,16 @@ struct Chain {
 #pragma unroll
       for (int rnd = 0; rnd < MR; ++rnd) {
         int pi = i, pj = j, t;
-        if (rnd < maxr) {
+        if constexpr (S == 4) {
+          // order <= 4: round r pairs x with x ^ (r + 1) (a complete
+          // round-robin of 4), so every partner element is a DPP lane swap
+          const int k = rnd + 1;
+          if (rnd < maxr && i < n && j < n) {  // pad lanes keep self
+            if ((i ^ k) < n) pi = i ^ k;
+            if ((j ^ k) < n) pj = j ^ k;
+          }
+          (void)t;
+        } else if (rnd < maxr) {
           if (i < n && jpair(i, rnd, m, n, t) >= 0) pi = t;
           if (j < n && jpair(j, rnd, m, n, t) >= 0) pj = t;
         }
@@ -1165,8 +1195,16 @@ struct Chain {
           const zc csj = bpermz(cs, acol[rnd]), ej = bpermz(e, acol[rnd]);
           const zc csi = bpermz(cs, arow[rnd]), ei = bpermz(e, arow[rnd]);
           const double shj = bperm(sh, acol[rnd]);
-          const zc g01 = bpermz(g, aipj[rnd]), g10 = bpermz(g, apij[rnd]), g11 = bpermz(g, apipj[rnd]);
-          const zc w1 = bpermz(w, aipj[rnd]);
+          zc g01, g10, g11, w1;
+          if constexpr (S == 4) {
+            g01 = xcol(g, rnd);  // G[i][j ^ k]
+            g10 = xrow(g, rnd);  // G[i ^ k][j]
+            g11 = xrow(g01, rnd);
+            w1 = xcol(w, rnd);
+          } else {
+            g01 = bpermz(g, aipj[rnd]); g10 = bpermz(g, apij[rnd]); g11 = bpermz(g, apipj[rnd]);
+            w1 = bpermz(w, aipj[rnd]);
+          }
           const bool rotj = (f & 8) && csj.y != 0.0, roti = (f & 16) && csi.y != 0.0;
           zc jjj, jpj, jii, jpi;
           jcol(f & 2, csj, ej, jjj, jpj);
