@@ -56,6 +56,14 @@ typedef struct ocg_info {
  * dH = sum_k 0.5 n_k(n_k-1) MPO data (:10-14) on `device`. */
 int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm,
                ocg_ctx** out);
+/* As ocg_create, choosing the engine: 0 auto (the single-workgroup LDS chain
+ * engine when the configuration fits it, else the HBM-resident engine),
+ * 1 LDS chain engine only (OCG_ECAP if it does not fit), 2 HBM-resident
+ * engine (multi-workgroup, MFMA-FP64 contractions; configurations such as
+ * L=20, p=7, chi=256).  Both engines implement every entry point below with
+ * the same arithmetic. */
+int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm, int engine,
+                  ocg_ctx** out);
 /* number of visible HIP devices (OCG_EHIP and *n = 0 without a GPU) */
 int ocg_device_count(int* n);
 int ocg_destroy(ocg_ctx* ctx);
@@ -77,6 +85,15 @@ int ocg_step(ocg_ctx* ctx, const int* dims, const double* data, double from, dou
 /* nsteps consecutive steps with controls u[0..nsteps] (step i: u[i] -> u[i+1]) */
 int ocg_steps(ocg_ctx* ctx, const int* dims, const double* data, const double* u, int nsteps, int forward,
               int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem);
+/* Batched BH_tDMRG::step over n independent states, one device launch
+ * (SURVEY.md §8b `ocg_step_batch`): state i = (dims + i*(L+1)*(Q+1), data[i])
+ * takes one step u_from[i] -> u_to[i] in direction `forward`; the result goes
+ * to (out_dims + i*(L+1)*(Q+1), out_data[i]) of capacity out_cap[i] complex
+ * elements, size in out_nelem[i].  Uses scratch slots after the trajectories
+ * (device psi_t / xi_t / xiH_t are left intact). */
+int ocg_step_batch(ocg_ctx* ctx, int n, const int* dims, const double* const* data, const double* u_from,
+                   const double* u_to, int forward, int* out_dims, double* const* out_data, const size_t* out_cap,
+                   size_t* out_nelem);
 /* overlapC(x, y) = <x|y> (with_dH = 0) or overlapC(x, propDeriv, y) = <x|dH|y>
  * (with_dH = 1) (src/OptimalControl.cpp:242, :412); out = {re, im} */
 int ocg_overlap(ocg_ctx* ctx, const int* dims_x, const double* x, const int* dims_y, const double* y,
@@ -132,7 +149,9 @@ int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_
  * Per-kernel HIP-event timing on the context's stream and the algorithmic
  * traffic model of DESIGN.md §Roofline.  kind: 0 trajectory, 1 overlaps,
  * 2 dH apply, 3 Hessian rows, 4 steps, 5 fused pipeline (ocg_hessian phase 1),
- * 6 batched row overlaps (ocg_hessian phase 2).  Sums since the last reset. */
+ * 6 batched row overlaps (ocg_hessian phase 2), 7 the HBM engine's MFMA GEMM
+ * kernel (k_gemm: HIP-event time, algorithmic bytes and flops of its tasks;
+ * zeros on the LDS engine).  Sums since the last reset. */
 int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
                      double* alg_flops, long* sweep_steps);
 int ocg_reset_stats(ocg_ctx* ctx);

@@ -39,7 +39,11 @@ struct OcgParams {
   int th2cap;               // two-site Θ elements bound (physical bonds)
   int nplan;                // decomposition plan slots in LDS (0: plans off)
   int plan_pe;              // Θ elements a plan slot can describe
+  int* err;                 // device error word of the context (bit 0: Jacobi sweep cap
+                            // reached, bit 1: pipeline watchdog); checked after every launch
 };
+#define OCG_ERR_JACOBI 1
+#define OCG_ERR_WATCHDOG 2
 
 // Truncation used for gauge moves and the left-to-right half of the dH
 // compression (ITensor MPS::position / orthogonalize; parity unpinned, the

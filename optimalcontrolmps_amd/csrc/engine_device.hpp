@@ -1235,6 +1235,7 @@ struct Chain {
         }
         if (done || __ballot(flag) == 0) break;
       }
+      if (sweep == 40 && lane == 0 && P.err) atomicOr(P.err, OCG_ERR_JACOBI);  // not converged: surfaced as OCG_ENUM
 #ifdef OCG_PROFILE
       if (tid == 0) { PROF[20] += sweep + 1; PROF[21] += 1.0; PROF[22] += maxr; }  // sweeps, calls, rounds/sweep
 #endif
@@ -1320,6 +1321,7 @@ struct Chain {
       const int more = ISCAL[fl];
       if (!more) break;
     }
+    if (sweep == 40 && tid == 0 && P.err) atomicOr(P.err, OCG_ERR_JACOBI);  // not converged: surfaced as OCG_ENUM
 #ifdef OCG_PROFILE
     if (tid == 0) { PROF[20] += sweep + 1; PROF[21] += 1.0; PROF[22] += maxr; }  // sweeps, calls, rounds/sweep
 #endif

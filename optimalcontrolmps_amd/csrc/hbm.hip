@@ -1,0 +1,1894 @@
+// Host side of the HBM-resident tDMRG engine (see hbm_device.hpp for the
+// kernels and DESIGN.md §9 for the data layout).  Restates, batched over many
+// MPS chains at once and with every tensor in HBM:
+//   BH_tDMRG::step / doStep                  (reference src/BH_tDMRG.cpp:111-230)
+//   ITensor denmatDecomp + truncate per QN   (called at src/BH_tDMRG.cpp:178,191,209)
+//   MPS::position / normalize                (src/BH_tDMRG.cpp:187,198,217,228)
+//   exactApplyMPO(propDeriv, psi)            (src/OptimalControl.cpp:256,302)
+//   overlapC(psi, phi) / overlapC(psi,H,phi) (src/OptimalControl.cpp:242,261,272,412)
+// with the same arithmetic choices as the LDS chain engine and the oracle
+// (Gram on the smaller side, ITensor truncation rule, gauge cutoff 1e-14).
+//
+// Site storage ("left-grouped"): site k holds, for every right sector q' of
+// bond k (ascending), the left matricisation Lmat_q' = rows (n, a in bond
+// k-1 sector q'-n) n-ascending, cols = bond-k states of sector q', row-major.
+// Block (q, n) of the site is therefore one contiguous row-major
+// dims[k-1][q] x dims[k][q+n] matrix (the interchange format's block, in a
+// different block order), Lmat_q' is contiguous, and the right
+// matricisation's column segments are those blocks.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hbm.hpp"
+#include "hbm_device.hpp"
+
+namespace hbm {
+
+// ---------------------------------------------------------------- errors
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+#define HCK(expr)                                                                                 \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) throw ::hbm::Error(3, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+constexpr double kGaugeCutoff = 1e-14;  // = OCG_GAUGE_CUTOFF of the LDS engine and the oracle
+constexpr int kNoMaxm = 1 << 30;
+
+// ---------------------------------------------------------------- dims / layouts
+struct Dims {
+  int L = 0, Q1 = 0;
+  std::vector<int> v;  // (L+1) * Q1
+  int operator()(int b, int q) const { return (q < 0 || q >= Q1) ? 0 : v[size_t(b) * Q1 + q]; }
+  int& at(int b, int q) { return v[size_t(b) * Q1 + q]; }
+  int bond(int b) const {
+    int s = 0;
+    for (int q = 0; q < Q1; ++q) s += v[size_t(b) * Q1 + q];
+    return s;
+  }
+};
+
+// offsets (in z) of site k's pieces for the given bond dims
+struct SiteLayout {
+  std::vector<long> lmat;   // [q'] offset of Lmat_q' (-1 if empty)
+  std::vector<int> lrows;   // [q'] rows of Lmat_q'
+  std::vector<int> rowoff;  // [q' * p + n] row of segment n inside Lmat_q' (-1 absent)
+  long size = 0;
+  // block (q, n): offset and leading dimension (= cols)
+  long blk(int q, int n, int p, const Dims& d, int k, int* ld = nullptr) const {
+    const int qq = q + n;
+    if (qq >= int(lmat.size()) || lmat[qq] < 0 || rowoff[qq * p + n] < 0 || d(k - 1, q) == 0) return -1;
+    const int c = d(k, qq);
+    if (ld) *ld = c;
+    return lmat[qq] + long(rowoff[qq * p + n]) * c;
+  }
+};
+static SiteLayout site_layout(const Dims& d, int k, int p) {
+  SiteLayout s;
+  const int Q1 = d.Q1;
+  s.lmat.assign(Q1, -1);
+  s.lrows.assign(Q1, 0);
+  s.rowoff.assign(size_t(Q1) * p, -1);
+  long off = 0;
+  for (int qq = 0; qq < Q1; ++qq) {
+    const int c = d(k, qq);
+    int r = 0;
+    for (int n = 0; n < p; ++n) {
+      const int dl = d(k - 1, qq - n);
+      if (dl > 0) { s.rowoff[qq * p + n] = r; r += dl; }
+    }
+    s.lrows[qq] = r;
+    if (c > 0 && r > 0) { s.lmat[qq] = off; off += long(r) * c; }
+  }
+  s.size = off;
+  return s;
+}
+
+// ---------------------------------------------------------------- device buffers
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HCK(hipMalloc(&p, sizeof(T) * n));
+    cap = n;
+  }
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// ---------------------------------------------------------------- MPS objects
+// A view of an MPS: bond dims + the device address of every site.
+struct View {
+  const Dims* d = nullptr;
+  std::array<z*, 64> site{};
+};
+
+// Chain: an MPS being propagated, two buffers per site (the new layout of a
+// site is written to its other buffer, then the two are swapped).
+struct Chain {
+  Dims dims;
+  std::vector<z*> buf[2];
+  std::vector<int> cur;
+  bool wide = false;
+  z* site(int k) const { return buf[cur[k]][k]; }
+  z* other(int k) const { return buf[1 - cur[k]][k]; }
+  void flip(int k) { cur[k] ^= 1; }
+  View view() const {
+    View v;
+    v.d = &dims;
+    for (size_t k = 1; k < cur.size(); ++k) v.site[k] = site(int(k));
+    return v;
+  }
+};
+
+// Stored state (trajectory slot): contiguous sites in site order.
+struct State {
+  Dims dims;
+  z* data = nullptr;
+  std::vector<long> off;  // [k] site offset
+  View view() const {
+    View v;
+    v.d = &dims;
+    for (size_t k = 1; k < off.size(); ++k) v.site[k] = data + off[k];
+    return v;
+  }
+};
+
+// ---------------------------------------------------------------- engine
+struct Engine {
+  // model
+  int L, p, Q, Q1;
+  double J, dt, cutoff;
+  int maxm;
+  int device;
+  std::vector<int> gate_i1;
+  std::vector<double> dH;
+  std::vector<int> md;   // (L+1)*Q1 Schmidt-rank bound per sector
+  std::vector<int> mdz;  // inside the dH zip-up: min(HS_left, 2 min(HS_left, HS_right))
+  std::vector<long long> hs_bond;  // total Hilbert-space bound per bond
+  // capacities (complex elements per site) of normal and wide (dH zip-up) chains
+  std::vector<int> bcap, bcapw;  // per bond
+  std::vector<long> scap, scapw;
+  long state_cap = 0;
+  // device
+  hipStream_t st = nullptr;
+  GateConst gcst{};
+  DBuf<z> d_gf, d_gb;
+  DBuf<z> chain_pool, chain_pool_w;
+  int nchain_cap = 0, nchain_cap_w = 0;
+  std::vector<int> free_chain, free_chain_w;
+  std::vector<std::unique_ptr<Chain>> chains;  // index = pool slot (normal), wide ones separate
+  std::vector<std::unique_ptr<Chain>> chains_w;
+  DBuf<z> heap;             // stored states
+  size_t heap_slots = 0;
+  std::vector<State> states;  // [slot]
+  // stats
+  double gemm_flops = 0, gemm_bytes = 0, gemm_ms = 0;
+  long gemm_launches = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> gemm_ev;
+  std::vector<hipEvent_t> ev_pool;
+  hipEvent_t ev_kept = nullptr;
+  double phase_ms[8] = {0};
+  long phase_n[8] = {0};
+  double steps_done[8] = {0};
+
+  Engine(int device_, int L_, int p_, int npart, double J_, double dt_, double cutoff_, int maxm_)
+      : L(L_), p(p_), Q(npart), Q1(npart + 1), J(J_), dt(dt_), cutoff(cutoff_),
+        maxm(maxm_ > 0 ? maxm_ : 5000), device(device_) {}
+  ~Engine() {
+    for (auto& e : ev_pool) (void)hipEventDestroy(e);
+    for (auto& e : gemm_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+    if (ev_kept) (void)hipEventDestroy(ev_kept);
+    if (st) (void)hipStreamDestroy(st);
+  }
+
+  // ------------------------------------------------------------ setup
+  void init(const std::vector<int>& md_in, const std::vector<int>& mdz_in, const std::vector<double>& gf,
+            const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal,
+            const std::vector<int>& gates) {
+    HCK(hipSetDevice(device));
+    thost.pinned = true;
+    HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
+    md = md_in;
+    mdz = mdz_in;
+    gate_i1 = gates;
+    dH.resize(p);
+    for (int n = 0; n < p; ++n) dH[n] = 0.5 * n * (n - 1);
+    set_gates(gf, gb, glo, gsz, goff, gtotal);
+    // bond capacities: Maxm (or the Hilbert-space bound) total per bond
+    hs_bond.assign(L + 1, 0);
+    for (int b = 0; b <= L; ++b) {
+      long long s = 0;
+      for (int q = 0; q < Q1; ++q) s += md[size_t(b) * Q1 + q];
+      hs_bond[b] = s;
+    }
+    set_caps(0);
+  }
+  void set_gates(const std::vector<double>& gf, const std::vector<double>& gb, const int* glo, const int* gsz,
+                 const int* goff, int gtotal) {
+    gcst.p = p;
+    gcst.Q1 = Q1;
+    for (int D = 0; D < 24; ++D) { gcst.glo[D] = glo[D]; gcst.gsz[D] = gsz[D]; gcst.goff[D] = goff[D]; }
+    d_gf.reserve(gtotal);
+    d_gb.reserve(gtotal);
+    HCK(hipMemcpy(d_gf.p, gf.data(), sizeof(z) * gtotal, hipMemcpyHostToDevice));
+    HCK(hipMemcpy(d_gb.p, gb.data(), sizeof(z) * gtotal, hipMemcpyHostToDevice));
+  }
+  // per-bond capacities from max(Maxm, widest state seen), capped by the
+  // Hilbert-space bound; chains and the state heap are sized from them
+  int widest = 0;
+  void set_caps(int wider) {
+    widest = std::max(widest, wider);
+    const long long want = std::max<long long>(maxm, widest);
+    std::vector<int> bc(L + 1), bw(L + 1);
+    for (int b = 0; b <= L; ++b) {
+      bc[b] = int(std::min<long long>(hs_bond[b], want));
+      bw[b] = (b == 0 || b == L) ? bc[b] : 2 * bc[b];  // the zip-up doubles every inner bond
+    }
+    if (bc == bcap && bw == bcapw) return;
+    // existing chains / states keep their buffers only if nothing grew
+    if (!chains.empty() || !chains_w.empty() || !states.empty()) {
+      bool grew = false;
+      for (int b = 0; b <= L; ++b)
+        if (bcap.size() && (bc[b] > bcap[b] || bw[b] > bcapw[b])) grew = true;
+      if (grew) throw Error(2, "state wider than the engine capacity fixed at ocg_set_states");
+      return;
+    }
+    bcap = bc;
+    bcapw = bw;
+    scap.assign(L + 1, 0);
+    scapw.assign(L + 1, 0);
+    state_cap = 0;
+    for (int k = 1; k <= L; ++k) {
+      scap[k] = std::max<long>(1, long(bcap[k - 1]) * bcap[k]);
+      scapw[k] = std::max<long>(1, long(bcapw[k - 1]) * bcapw[k]);
+      state_cap += scap[k];
+    }
+  }
+  long chain_elems(bool wide) const {
+    long s = 0;
+    for (int k = 1; k <= L; ++k) s += 2 * (wide ? scapw[k] : scap[k]);
+    return s;
+  }
+  size_t mps_max_nelem() const { return size_t(state_cap); }
+
+  // ------------------------------------------------------------ chains
+  void reserve_chains(int n, bool wide) {
+    auto& pool = wide ? chain_pool_w : chain_pool;
+    auto& capn = wide ? nchain_cap_w : nchain_cap;
+    auto& vec = wide ? chains_w : chains;
+    auto& fr = wide ? free_chain_w : free_chain;
+    if (n <= capn) return;
+    if (capn > 0) {
+      // grow: keep it simple, every chain must be free (batches allocate at their start)
+      if (int(fr.size()) != capn) throw Error(4, "internal: chain pool grown while chains are in use");
+      sync();
+    }
+    const long per = chain_elems(wide);
+    pool.reserve(size_t(per) * n);
+    vec.clear();
+    fr.clear();
+    for (int i = 0; i < n; ++i) {
+      auto c = std::make_unique<Chain>();
+      c->wide = wide;
+      c->buf[0].assign(L + 1, nullptr);
+      c->buf[1].assign(L + 1, nullptr);
+      c->cur.assign(L + 1, 0);
+      z* b = pool.p + size_t(per) * i;
+      for (int k = 1; k <= L; ++k) {
+        const long sc = wide ? scapw[k] : scap[k];
+        c->buf[0][k] = b; b += sc;
+        c->buf[1][k] = b; b += sc;
+      }
+      vec.push_back(std::move(c));
+      fr.push_back(n - 1 - i);
+    }
+    capn = n;
+  }
+  Chain* acquire(bool wide) {
+    auto& fr = wide ? free_chain_w : free_chain;
+    if (fr.empty()) throw Error(4, "internal: chain pool exhausted");
+    const int i = fr.back();
+    fr.pop_back();
+    Chain* c = (wide ? chains_w : chains)[i].get();
+    std::fill(c->cur.begin(), c->cur.end(), 0);
+    return c;
+  }
+  void release(Chain* c) {
+    auto& vec = c->wide ? chains_w : chains;
+    for (size_t i = 0; i < vec.size(); ++i)
+      if (vec[i].get() == c) { (c->wide ? free_chain_w : free_chain).push_back(int(i)); return; }
+  }
+
+  // ------------------------------------------------------------ states
+  void reserve_states(size_t nslots) {
+    if (nslots <= heap_slots) return;
+    // keep the contents: copy into the new heap
+    DBuf<z> nh;
+    nh.reserve(size_t(state_cap) * nslots);
+    if (heap_slots) HCK(hipMemcpyAsync(nh.p, heap.p, sizeof(z) * state_cap * heap_slots, hipMemcpyDeviceToDevice, st));
+    sync();
+    std::swap(heap.p, nh.p);
+    std::swap(heap.cap, nh.cap);
+    for (size_t s = 0; s < states.size(); ++s) states[s].data = heap.p + size_t(state_cap) * s;
+    states.resize(nslots);
+    for (size_t s = heap_slots; s < nslots; ++s) {
+      states[s].data = heap.p + size_t(state_cap) * s;
+      states[s].dims.L = L;
+      states[s].dims.Q1 = Q1;
+      states[s].dims.v.assign(size_t(L + 1) * Q1, 0);
+      states[s].off.assign(L + 1, 0);
+    }
+    heap_slots = nslots;
+  }
+  void set_state_layout(State& s) {
+    long o = 0;
+    for (int k = 1; k <= L; ++k) {
+      s.off[k] = o;
+      o += site_layout(s.dims, k, p).size;
+    }
+    if (o > state_cap) throw Error(2, "state exceeds the slot capacity");
+  }
+
+  // ------------------------------------------------------------ arenas
+  // Workspace and task uploads are bump-allocated from chunked arenas (device
+  // blocks, pinned host staging) and recycled at every stream
+  // synchronisation: nothing queued can still read them then.  Chunks are
+  // kept across phases, so steady-state allocation is free.
+  struct Arena {
+    std::vector<std::pair<char*, size_t>> blk;
+    size_t bi = 0, top = 0;
+    bool pinned = false;
+    char* get(size_t bytes) {
+      bytes = (bytes + 255) & ~size_t(255);
+      while (bi < blk.size() && top + bytes > blk[bi].second) { ++bi; top = 0; }
+      if (bi == blk.size()) {
+        const size_t sz = std::max<size_t>(bytes, blk.empty() ? (size_t(8) << 20) : 2 * blk.back().second);
+        char* ptr = nullptr;
+        if (pinned) HCK(hipHostMalloc((void**)&ptr, sz, hipHostMallocDefault));
+        else HCK(hipMalloc((void**)&ptr, sz));
+        blk.push_back({ptr, sz});
+        top = 0;
+      }
+      char* r = blk[bi].first + top;
+      top += bytes;
+      return r;
+    }
+    void reset() { bi = 0; top = 0; }
+    ~Arena() {
+      for (auto& b : blk) {
+        if (pinned) (void)hipHostFree(b.first);
+        else (void)hipFree(b.first);
+      }
+    }
+  };
+  Arena work, tdev, thost;
+  void sync() {
+    HCK(hipStreamSynchronize(st));
+    resolve_timers();
+    work.reset();
+    tdev.reset();
+    thost.reset();
+  }
+  template <class T>
+  T* walloc(size_t n) {
+    return (T*)work.get(sizeof(T) * std::max<size_t>(n, 1));
+  }
+  template <class T>
+  const T* upload(const std::vector<T>& v) {
+    if (v.empty()) return nullptr;
+    const size_t bytes = sizeof(T) * v.size();
+    char* h = thost.get(bytes);
+    char* d = tdev.get(bytes);
+    std::memcpy(h, v.data(), bytes);
+    HCK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    return (const T*)d;
+  }
+
+  // ------------------------------------------------------------ launches
+  hipEvent_t get_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HCK(hipEventCreate(&e));
+    return e;
+  }
+  void resolve_timers() {
+    for (auto& pr : gemm_ev) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) gemm_ms += ms;
+      ev_pool.push_back(pr.first);
+      ev_pool.push_back(pr.second);
+    }
+    gemm_ev.clear();
+  }
+  // GEMM tasks: drop empty outputs, prefix the tiles, account flops/bytes
+  void gemm(std::vector<GTask>& tasks, const std::vector<GSeg>& segs) {
+    std::vector<GTask> t;
+    t.reserve(tasks.size());
+    int tiles = 0;
+    for (auto& x : tasks) {
+      if (x.m <= 0 || x.n <= 0) continue;
+      x.tile0 = tiles;
+      tiles += ((x.m + GT - 1) / GT) * ((x.n + GT - 1) / GT);
+      for (int s = 0; s < x.nseg; ++s) {
+        const GSeg& g = segs[x.seg0 + s];
+        gemm_flops += 8.0 * x.m * x.n * g.k;
+        gemm_bytes += 16.0 * (double(x.m) * g.k + double(g.k) * x.n);
+      }
+      gemm_bytes += 16.0 * x.m * x.n;
+      t.push_back(x);
+    }
+    tasks.clear();
+    if (t.empty()) return;
+    const GTask* dt_ = upload(t);
+    const GSeg* ds = upload(segs);
+    hipEvent_t a = get_event(), b = get_event();
+    HCK(hipEventRecord(a, st));
+    hipLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, dt_, int(t.size()), ds);
+    HCK(hipGetLastError());
+    HCK(hipEventRecord(b, st));
+    gemm_ev.push_back({a, b});
+    ++gemm_launches;
+  }
+  void copy(std::vector<CTask>& tasks) {
+    std::vector<CTask> t;
+    long long tot = 0;
+    for (auto& x : tasks) {
+      if (x.rows <= 0 || x.cols <= 0) continue;
+      x.e0 = tot;
+      tot += (long long)x.rows * x.cols;
+      t.push_back(x);
+    }
+    tasks.clear();
+    if (t.empty()) return;
+    const CTask* d = upload(t);
+    const long long blocks = std::min<long long>((tot + NT - 1) / NT, 8192);
+    hipLaunchKernelGGL(k_copy, dim3(unsigned(blocks)), dim3(NT), 0, st, d, int(t.size()), tot);
+    HCK(hipGetLastError());
+  }
+  static CTask ctask(const z* src, z* dst, int rows, int cols, int lds, int ldd, int mode = 0) {
+    CTask c{};
+    c.src = src; c.dst = dst; c.rows = rows; c.cols = cols; c.lds = lds; c.ldd = ldd; c.mode = mode;
+    c.f = mk(1, 0);
+    return c;
+  }
+  static GTask gtask(z* C, int ldc, int m, int n, int seg0, int nseg) {
+    GTask t{};
+    t.C = C; t.ldc = ldc; t.m = m; t.n = n; t.seg0 = seg0; t.nseg = nseg;
+    return t;
+  }
+  static GSeg gseg(const z* A, int lda, const z* B, int ldb, int k, int ops, double alpha = 1.0) {
+    GSeg s{};
+    s.A = A; s.B = B; s.lda = lda; s.ldb = ldb; s.k = k; s.ops = ops; s.alpha = alpha;
+    return s;
+  }
+
+  // ------------------------------------------------------------ decomposition
+  // One QN-blocked matrix per chain: sector q is R_q x C_q given as column
+  // segments (each: pointer, leading dimension, width); rows contiguous.
+  struct Seg {
+    const z* ptr;
+    int ld, c0, nc;
+  };
+  struct QMat {
+    std::vector<int> R, C;
+    std::vector<std::vector<Seg>> segs;  // [q]
+  };
+  // Result of one decomposition of one chain: per sector kept k_q and the
+  // factors X (R x k, ld k) and Y (k x C, ld C), written where the caller
+  // asked (dest pointers per sector; Y as column segments).
+  struct Dest {
+    std::vector<z*> X;                       // [q] (ld k_q); null: scratch
+    std::vector<std::vector<z*>> Y;          // [q][seg] destination of Y's column segment (ld = segment width)
+  };
+  enum { kFromleft = 0, kFromright = 1 };
+
+  struct DecompJob {
+    QMat M;
+    int dir;
+    double cutoff;
+    int maxm;
+    int normalize;
+    const int* bound;  // host array of per-sector bounds (Q1)
+    // outputs (filled by decompose)
+    std::vector<int> kept;
+    std::vector<z*> X;  // scratch factors when no destination
+    std::vector<z*> Y;
+  };
+
+  // Stage 1: Gram + eigenvalues + truncation; returns after the host knows
+  // every kept count.  Stage 2 (factors) runs from decompose_factors.
+  struct EigRun {
+    std::vector<EProb> probs;
+    std::vector<int> prob_job, prob_q;
+    std::vector<int> side;  // per problem: 0 rows (M M^H), 1 cols (M^H M)
+    int* d_kept = nullptr;
+    double* d_keptw = nullptr;  // [job][2]
+    std::vector<int> h_kept;
+    std::vector<double> h_keptw;
+    std::vector<int> job_p0;
+    const EProb* d_probs = nullptr;
+  };
+
+  void decompose_eig(std::vector<DecompJob>& jobs, EigRun& R) {
+    // problems and workspace
+    size_t need = 0;
+    for (auto& J : jobs)
+      for (int q = 0; q < Q1; ++q) {
+        const int Rq = J.M.R[q], Cq = J.M.C[q];
+        if (Rq <= 0 || Cq <= 0) continue;
+        const size_t n = size_t(std::min(Rq, Cq));
+        need += (sizeof(z) * (2 * n * n + 2 * n) + sizeof(double) * (2 * n * n + 5 * n) + 4096);
+      }
+    need += sizeof(int) * 64 * (jobs.size() + 1) * Q1 + sizeof(double) * 2 * jobs.size() + 4096;
+    R.probs.clear();
+    R.prob_job.clear();
+    R.prob_q.clear();
+    R.side.clear();
+    R.job_p0.assign(jobs.size() + 1, 0);
+    int np = 0;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      R.job_p0[j] = np;
+      for (int q = 0; q < Q1; ++q)
+        if (jobs[j].M.R[q] > 0 && jobs[j].M.C[q] > 0) ++np;
+    }
+    R.job_p0[jobs.size()] = np;
+    R.d_kept = walloc<int>(std::max(np, 1));
+    R.d_keptw = walloc<double>(2 * std::max<size_t>(jobs.size(), 1));
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    std::vector<TItem> items;
+    std::vector<int> bounds;
+    bounds.reserve(np);
+    int pi = 0;
+    int maxn = 1, maxT = 0;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      DecompJob& J = jobs[j];
+      int T = 0;
+      for (int q = 0; q < Q1; ++q) {
+        const int Rq = J.M.R[q], Cq = J.M.C[q];
+        if (Rq <= 0 || Cq <= 0) continue;
+        const int n = std::min(Rq, Cq);
+        const int sd = Rq <= Cq ? 0 : 1;
+        EProb P{};
+        P.n = n;
+        P.q = q;
+        P.A = walloc<z>(size_t(n) * n);
+        P.U = walloc<z>(size_t(n) * n);
+        P.ph = walloc<z>(n);
+        P.d = walloc<double>(n);
+        P.e = walloc<double>(n);
+        P.tau = walloc<double>(n);
+        P.w = walloc<double>(n);
+        P.Z = walloc<double>(size_t(n) * n);
+        P.Dv = walloc<double>(size_t(n) * n);
+        P.kept = R.d_kept + pi;
+        R.probs.push_back(P);
+        R.prob_job.push_back(int(j));
+        R.prob_q.push_back(q);
+        R.side.push_back(sd);
+        bounds.push_back(J.bound[q]);
+        maxn = std::max(maxn, n);
+        T += n;
+        // Gram: rows side G = M M^H = sum_seg S S^H; cols side G[seg a][seg b] = S_a^H S_b
+        const auto& SG = J.M.segs[q];
+        if (sd == 0) {
+          const int s0 = int(gs.size());
+          for (auto& s : SG) gs.push_back(gseg(s.ptr, s.ld, s.ptr, s.ld, s.nc, 2));
+          gt.push_back(gtask(P.A, n, n, n, s0, int(SG.size())));
+        } else {
+          for (auto& a : SG)
+            for (auto& b : SG) {
+              const int s0 = int(gs.size());
+              gs.push_back(gseg(a.ptr, a.ld, b.ptr, b.ld, Rq, 1));
+              gt.push_back(gtask(P.A + size_t(a.c0) * n + b.c0, n, a.nc, b.nc, s0, 1));
+            }
+        }
+        ++pi;
+      }
+      if (T > kMaxEig) throw Error(2, "decomposition with more eigenvalues than k_truncate holds");
+      maxT = std::max(maxT, T);
+      TItem I{};
+      I.p0 = R.job_p0[j];
+      I.np = R.job_p0[j + 1] - R.job_p0[j];
+      I.cutoff = J.cutoff;
+      I.maxm = J.maxm;
+      I.normalize = J.normalize;
+      I.kept = R.d_kept + I.p0;
+      I.keptw = R.d_keptw + 2 * j;
+      items.push_back(I);
+    }
+    if (np == 0) {
+      for (auto& J : jobs) J.kept.assign(Q1, 0);
+      return;
+    }
+    gemm(gt, gs);
+    R.d_probs = upload(R.probs);
+    // bounds: device copy, then point the items at it
+    const int* d_bounds = upload(bounds);
+    for (auto& I : items) I.bound = d_bounds + I.p0;
+    const TItem* d_items = upload(items);
+    // eigenvalues (LDS: 3 complex + 2 real vectors, plus the Gram block if small)
+    int lds_v = 64;
+    for (auto& P : R.probs) lds_v = std::max(lds_v, 64 * P.n + (P.n <= kLdsOrder ? 16 * P.n * P.n : 0) + 64);
+    hipLaunchKernelGGL(k_heev_vals, dim3(np), dim3(NT), lds_v, st, R.d_probs, np);
+    HCK(hipGetLastError());
+    int maxnp = 0;
+    for (auto& I : items) maxnp = std::max(maxnp, I.np);
+    hipLaunchKernelGGL(k_truncate, dim3(int(items.size())), dim3(NT), truncate_lds(maxnp), st, d_items, R.d_probs);
+    HCK(hipGetLastError());
+    R.h_kept.assign(np, 0);
+    R.h_keptw.assign(2 * jobs.size(), 0.0);
+    HCK(hipMemcpyAsync(R.h_kept.data(), R.d_kept, sizeof(int) * np, hipMemcpyDeviceToHost, st));
+    HCK(hipMemcpyAsync(R.h_keptw.data(), R.d_keptw, sizeof(double) * 2 * jobs.size(), hipMemcpyDeviceToHost, st));
+    HCK(hipEventRecord(ev_kept, st));
+    // eigenvectors of the kept eigenvalues (reads the kept counts on the device)
+    const int lds_e = 24 * maxn + 64;
+    hipLaunchKernelGGL(k_heev_vecs, dim3(np), dim3(NT), lds_e, st, R.d_probs, np);
+    HCK(hipGetLastError());
+    HCK(hipEventSynchronize(ev_kept));
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      jobs[j].kept.assign(Q1, 0);
+      for (int i = R.job_p0[j]; i < R.job_p0[j + 1]; ++i) jobs[j].kept[R.prob_q[i]] = R.h_kept[i];
+    }
+    (void)maxT;
+  }
+
+  // Factors of every job: X (R x k) and Y (k x C) per sector.  xdst[j][q]:
+  // destination of X (ld k) or null (scratch allocated here, returned in
+  // job.X); ydst[j][q][seg]: destination of Y's column segment (ld = its
+  // width) or empty (scratch, job.Y with ld C).
+  void decompose_factors(std::vector<DecompJob>& jobs, EigRun& R, const std::vector<std::vector<z*>>& xdst,
+                         const std::vector<std::vector<std::vector<z*>>>& ydst) {
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    std::vector<CTask> ct;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      DecompJob& J = jobs[j];
+      J.X.assign(Q1, nullptr);
+      J.Y.assign(Q1, nullptr);
+      const double* inv = R.d_keptw + 2 * j + 1;
+      for (int i = R.job_p0[j]; i < R.job_p0[j + 1]; ++i) {
+        const int q = R.prob_q[i], k = J.kept[q];
+        if (k <= 0) continue;
+        const EProb& P = R.probs[i];
+        const int Rq = J.M.R[q], Cq = J.M.C[q];
+        const auto& SG = J.M.segs[q];
+        z* X = (xdst.size() > j && xdst[j][q]) ? xdst[j][q] : walloc<z>(size_t(Rq) * k);
+        J.X[q] = X;
+        const bool ysplit = ydst.size() > j && !ydst[j][q].empty();
+        z* Ys = ysplit ? nullptr : walloc<z>(size_t(k) * Cq);
+        J.Y[q] = Ys;
+        auto ydest = [&](size_t s, int& ld) -> z* {
+          if (ysplit) { ld = SG[s].nc; return ydst[j][q][s]; }
+          ld = Cq;
+          return Ys + SG[s].c0;
+        };
+        if (R.side[i] == 0) {
+          // U: eigenvectors of M M^H (R x k).  X = U [Fromright: * sigma inv]
+          CTask c = ctask(P.U, X, Rq, k, k, k);
+          if (J.dir == kFromright) { c.cs = P.w; c.smode = 1 << 2; c.sc = inv; }
+          ct.push_back(c);
+          // Y = U^H M [Fromleft: * inv; Fromright: / sigma per row], per column segment
+          for (size_t s = 0; s < SG.size(); ++s) {
+            int ld;
+            z* Yd = ydest(s, ld);
+            const int s0 = int(gs.size());
+            gs.push_back(gseg(P.U, k, SG[s].ptr, SG[s].ld, Rq, 1));
+            GTask t = gtask(Yd, ld, k, SG[s].nc, s0, 1);
+            if (J.dir == kFromleft) t.sc = inv;
+            else { t.rs = P.w; t.smode = 2; }
+            gt.push_back(t);
+          }
+        } else {
+          // W: eigenvectors of M^H M (C x k).  Y = W^H [Fromleft: * sigma inv]
+          for (size_t s = 0; s < SG.size(); ++s) {
+            int ld;
+            z* Yd = ydest(s, ld);
+            CTask c = ctask(P.U + size_t(SG[s].c0) * k, Yd, k, SG[s].nc, k, ld, 1);
+            if (J.dir == kFromleft) { c.rs = P.w; c.smode = 1; c.sc = inv; }
+            ct.push_back(c);
+          }
+          // X = M W [Fromleft: / sigma per column; Fromright: * inv]
+          const int s0 = int(gs.size());
+          for (auto& s : SG) gs.push_back(gseg(s.ptr, s.ld, P.U + size_t(s.c0) * k, k, s.nc, 0));
+          GTask t = gtask(X, k, Rq, k, s0, int(SG.size()));
+          if (J.dir == kFromleft) { t.cs = P.w; t.smode = 2 << 2; }
+          else t.sc = inv;
+          gt.push_back(t);
+        }
+      }
+    }
+    copy(ct);
+    gemm(gt, gs);
+  }
+
+  // ------------------------------------------------------------ matricisations
+  // Lmat of site k (rows (n, a), cols bond-k sector q): contiguous
+  QMat lmat_of(const View& v, int k) const {
+    const Dims& d = *v.d;
+    SiteLayout sl = site_layout(d, k, p);
+    QMat M;
+    M.R.assign(Q1, 0);
+    M.C.assign(Q1, 0);
+    M.segs.assign(Q1, {});
+    for (int q = 0; q < Q1; ++q) {
+      if (sl.lmat[q] < 0) continue;
+      M.R[q] = sl.lrows[q];
+      M.C[q] = d(k, q);
+      M.segs[q].push_back(Seg{v.site[k] + sl.lmat[q], d(k, q), 0, d(k, q)});
+    }
+    return M;
+  }
+  // Rmat of site k (rows bond k-1 sector q, cols (n, c)): blocks as segments
+  QMat rmat_of(const View& v, int k) const {
+    const Dims& d = *v.d;
+    SiteLayout sl = site_layout(d, k, p);
+    QMat M;
+    M.R.assign(Q1, 0);
+    M.C.assign(Q1, 0);
+    M.segs.assign(Q1, {});
+    for (int q = 0; q < Q1; ++q) {
+      const int r = d(k - 1, q);
+      if (r == 0) continue;
+      int c = 0;
+      for (int n = 0; n < p && q + n < Q1; ++n) {
+        int ld;
+        const long o = sl.blk(q, n, p, d, k, &ld);
+        if (o < 0) continue;
+        M.segs[q].push_back(Seg{v.site[k] + o, ld, c, ld});
+        c += ld;
+      }
+      if (c == 0) { M.segs[q].clear(); continue; }
+      M.R[q] = r;
+      M.C[q] = c;
+    }
+    return M;
+  }
+  const int* bound_row(int b, bool zip) const { return (zip ? mdz.data() : md.data()) + size_t(b) * Q1; }
+
+  // ------------------------------------------------------------ gauge moves
+  // MPS::position one site right / left for a batch (cutoff/maxm/normalize
+  // as given; the gauge moves of doStep and exactApplyMPO use 1e-14, no Maxm).
+  void move_right(std::vector<Chain*>& cs, int k, double cut, int mm, bool zip) {
+    std::vector<DecompJob> jobs(cs.size());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      jobs[i].M = lmat_of(cs[i]->view(), k);
+      jobs[i].dir = kFromleft;
+      jobs[i].cutoff = cut;
+      jobs[i].maxm = mm;
+      jobs[i].normalize = 0;
+      jobs[i].bound = bound_row(k, zip);
+    }
+    EigRun R;
+    decompose_eig(jobs, R);
+    // new bond k dims -> new layouts of sites k and k+1
+    std::vector<std::vector<z*>> xdst(cs.size(), std::vector<z*>(Q1, nullptr));
+    std::vector<Dims> nd(cs.size());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      nd[i] = cs[i]->dims;
+      for (int q = 0; q < Q1; ++q) nd[i].at(k, q) = jobs[i].kept[q];
+      SiteLayout sl = site_layout(nd[i], k, p);
+      for (int q = 0; q < Q1; ++q)
+        if (jobs[i].kept[q] > 0 && sl.lmat[q] >= 0) xdst[i][q] = cs[i]->other(k) + sl.lmat[q];
+    }
+    decompose_factors(jobs, R, xdst, {});
+    // site k+1 <- Y * site k+1, block by block
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const Dims& od = cs[i]->dims;
+      SiteLayout so = site_layout(od, k + 1, p), sn = site_layout(nd[i], k + 1, p);
+      for (int q = 0; q < Q1; ++q) {
+        const int kq = jobs[i].kept[q];
+        if (kq <= 0) continue;
+        for (int n = 0; n < p && q + n < Q1; ++n) {
+          int ldo, ldn;
+          const long oo = so.blk(q, n, p, od, k + 1, &ldo), on = sn.blk(q, n, p, nd[i], k + 1, &ldn);
+          if (oo < 0 || on < 0) continue;
+          const int s0 = int(gs.size());
+          gs.push_back(gseg(jobs[i].Y[q], od(k, q), cs[i]->site(k + 1) + oo, ldo, od(k, q), 0));
+          gt.push_back(gtask(cs[i]->other(k + 1) + on, ldn, kq, ldn, s0, 1));
+        }
+      }
+    }
+    gemm(gt, gs);
+    for (size_t i = 0; i < cs.size(); ++i) {
+      cs[i]->dims = nd[i];
+      cs[i]->flip(k);
+      cs[i]->flip(k + 1);
+    }
+  }
+  void move_left(std::vector<Chain*>& cs, int k, double cut, int mm, bool zip) {
+    std::vector<DecompJob> jobs(cs.size());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      jobs[i].M = rmat_of(cs[i]->view(), k);
+      jobs[i].dir = kFromright;
+      jobs[i].cutoff = cut;
+      jobs[i].maxm = mm;
+      jobs[i].normalize = 0;
+      jobs[i].bound = bound_row(k - 1, zip);
+    }
+    EigRun R;
+    decompose_eig(jobs, R);
+    std::vector<std::vector<std::vector<z*>>> ydst(cs.size(), std::vector<std::vector<z*>>(Q1));
+    std::vector<Dims> nd(cs.size());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      nd[i] = cs[i]->dims;
+      for (int q = 0; q < Q1; ++q) nd[i].at(k - 1, q) = jobs[i].kept[q];
+      SiteLayout sl = site_layout(nd[i], k, p);
+      for (int q = 0; q < Q1; ++q) {
+        if (jobs[i].kept[q] <= 0) continue;
+        auto& segs = jobs[i].M.segs[q];
+        // the segments are the blocks (q, n) with both dims nonzero, in n order
+        for (int n = 0; n < p && q + n < Q1; ++n) {
+          int ld;
+          const long o = sl.blk(q, n, p, nd[i], k, &ld);
+          if (o < 0) continue;
+          ydst[i][q].push_back(cs[i]->other(k) + o);
+        }
+        if (ydst[i][q].size() != segs.size()) throw Error(4, "internal: right-matricisation segment mismatch");
+      }
+    }
+    decompose_factors(jobs, R, {}, ydst);
+    // site k-1 <- site k-1 * X, block by block
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const Dims& od = cs[i]->dims;
+      SiteLayout so = site_layout(od, k - 1, p), sn = site_layout(nd[i], k - 1, p);
+      for (int ql = 0; ql < Q1; ++ql)
+        for (int n = 0; n < p && ql + n < Q1; ++n) {
+          const int q = ql + n, kq = jobs[i].kept[q];
+          if (kq <= 0) continue;
+          int ldo, ldn;
+          const long oo = so.blk(ql, n, p, od, k - 1, &ldo), on = sn.blk(ql, n, p, nd[i], k - 1, &ldn);
+          if (oo < 0 || on < 0) continue;
+          const int s0 = int(gs.size());
+          gs.push_back(gseg(cs[i]->site(k - 1) + oo, ldo, jobs[i].X[q], kq, ldo, 0));
+          gt.push_back(gtask(cs[i]->other(k - 1) + on, ldn, od(k - 2, ql), kq, s0, 1));
+        }
+    }
+    gemm(gt, gs);
+    for (size_t i = 0; i < cs.size(); ++i) {
+      cs[i]->dims = nd[i];
+      cs[i]->flip(k);
+      cs[i]->flip(k - 1);
+    }
+  }
+  void position(std::vector<Chain*>& cs, int& centre, int target) {
+    while (centre < target) { move_right(cs, centre, kGaugeCutoff, kNoMaxm, false); ++centre; }
+    while (centre > target) { move_left(cs, centre, kGaugeCutoff, kNoMaxm, false); --centre; }
+  }
+
+  // ------------------------------------------------------------ site phases / norms
+  // site k of every chain times ph(chain, n) (U gates; doStep :133-136, :222-223)
+  void site_phase(std::vector<Chain*>& cs, int k, const std::vector<double>& u, const std::vector<double>& tau,
+                  const std::vector<double>* inv_norm) {
+    std::vector<CTask> ct;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const Dims& d = cs[i]->dims;
+      SiteLayout sl = site_layout(d, k, p);
+      for (int q = 0; q < Q1; ++q)
+        for (int n = 0; n < p && q + n < Q1; ++n) {
+          int ld;
+          const long o = sl.blk(q, n, p, d, k, &ld);
+          if (o < 0) continue;
+          z* b = cs[i]->site(k) + o;
+          CTask c = ctask(b, b, d(k - 1, q), ld, ld, ld);
+          const double a = -0.25 * u[i] * tau[i] * n * (n - 1);
+          c.f = mk(std::cos(a), std::sin(a));
+          if (inv_norm) c.f = mk(c.f.x * (*inv_norm)[i], c.f.y * (*inv_norm)[i]);
+          ct.push_back(c);
+        }
+    }
+    copy(ct);
+  }
+  // |site k|^2 of every view (one reduction launch, host readback)
+  std::vector<double> site_norm2(const std::vector<View>& vs, int k) {
+    double* acc = walloc<double>(vs.size());
+    HCK(hipMemsetAsync(acc, 0, sizeof(double) * vs.size(), st));
+    std::vector<CTask> ct;
+    for (size_t i = 0; i < vs.size(); ++i) {
+      const Dims& d = *vs[i].d;
+      SiteLayout sl = site_layout(d, k, p);
+      for (int q = 0; q < Q1; ++q) {
+        if (sl.lmat[q] < 0) continue;
+        CTask c = ctask(vs[i].site[k] + sl.lmat[q], nullptr, sl.lrows[q], d(k, q), d(k, q), 0, 4);
+        c.acc = acc + i;
+        ct.push_back(c);
+      }
+    }
+    copy(ct);
+    std::vector<double> h(vs.size());
+    HCK(hipMemcpyAsync(h.data(), acc, sizeof(double) * vs.size(), hipMemcpyDeviceToHost, st));
+    sync();
+    return h;
+  }
+
+  // ------------------------------------------------------------ step
+  // BH_tDMRG::step for a batch: chain i takes u_from[i] -> u_to[i] in
+  // direction fwd[i] (src/BH_tDMRG.cpp:111-230, as the oracle restates it)
+  void step(std::vector<Chain*>& cs, const std::vector<double>& uf, const std::vector<double>& ut,
+            const std::vector<int>& fwd) {
+    if (cs.empty()) return;
+    const size_t B = cs.size();
+    std::vector<double> tau(B);
+    for (size_t i = 0; i < B; ++i) tau[i] = fwd[i] ? dt : -dt;
+    if (L % 2 != 0) site_phase(cs, L, uf, tau, nullptr);  // lonely U_from on site L (:133-136)
+    int centre = 1;
+    bool fromLeft = true;
+    const int ng = int(gate_i1.size());
+    for (int g = 0; g < ng; ++g) {
+      const int i1 = gate_i1[g], i2 = i1 + 1;
+      const int mode = fromLeft ? 0 : 1;
+      const bool lonely = fromLeft && i2 == L && L % 2 == 0;  // (:153-155)
+      std::vector<ThetaJob> th(B);
+      build_theta(cs, i1, th);
+      apply_gate(cs, th, i1, uf, ut, tau, fwd, mode, lonely);
+      if (g + 1 < ng) {
+        const int ni1 = gate_i1[g + 1], ni2 = ni1 + 1;
+        if (ni1 >= i2) {
+          two_site(cs, th, i1, kFromleft);
+          centre = i1 + 1;
+          position(cs, centre, ni1);
+        } else {
+          two_site(cs, th, i1, kFromright);
+          centre = i1;
+          position(cs, centre, ni2);
+        }
+        if (i2 == ni1 || i1 == ni2) fromLeft = false;
+      } else {
+        two_site(cs, th, i1, kFromright);
+        centre = i1;
+        position(cs, centre, 1);
+      }
+      sync();
+    }
+    // U_to on site 1 (:222-223) and psi.normalize() (:228)
+    std::vector<View> vs;
+    for (auto* c : cs) vs.push_back(c->view());
+    std::vector<double> n2 = site_norm2(vs, 1);
+    std::vector<double> inv(B);
+    for (size_t i = 0; i < B; ++i) inv[i] = n2[i] > 0 ? 1.0 / std::sqrt(n2[i]) : 1.0;
+    site_phase(cs, 1, ut, tau, &inv);
+    sync();
+  }
+
+  struct ThetaJob {
+    z* th = nullptr;
+    std::vector<long> thoff;
+    std::vector<int> R, C, ro, co;  // ro/co: [q * p + n]
+  };
+  // Θ_q = Lmat(A_i1)_q * Rmat(A_i2)_q for every middle sector q (zero where
+  // the middle sector is empty)
+  void build_theta(std::vector<Chain*>& cs, int i1, std::vector<ThetaJob>& th) {
+    size_t need = 0;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const Dims& d = cs[i]->dims;
+      for (int q = 0; q < Q1; ++q) {
+        long R = 0, C = 0;
+        for (int n = 0; n < p; ++n) { R += d(i1 - 1, q - n); if (q + n < Q1) C += d(i1 + 1, q + n); }
+        need += sizeof(z) * R * C + 256;
+      }
+    }
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const Dims& d = cs[i]->dims;
+      ThetaJob& T = th[i];
+      T.thoff.assign(Q1, 0);
+      T.R.assign(Q1, 0);
+      T.C.assign(Q1, 0);
+      T.ro.assign(size_t(Q1) * p, -1);
+      T.co.assign(size_t(Q1) * p, -1);
+      long tot = 0;
+      for (int q = 0; q < Q1; ++q) {
+        int R = 0, C = 0;
+        for (int n = 0; n < p; ++n) {
+          if (d(i1 - 1, q - n) > 0) { T.ro[q * p + n] = R; R += d(i1 - 1, q - n); }
+          if (q + n < Q1 && d(i1 + 1, q + n) > 0) { T.co[q * p + n] = C; C += d(i1 + 1, q + n); }
+        }
+        T.R[q] = R;
+        T.C[q] = C;
+        T.thoff[q] = tot;
+        if (R > 0 && C > 0) tot += long(R) * C;
+      }
+      T.th = walloc<z>(std::max<long>(tot, 1));
+      SiteLayout s1 = site_layout(d, i1, p), s2 = site_layout(d, i1 + 1, p);
+      for (int q = 0; q < Q1; ++q) {
+        if (T.R[q] == 0 || T.C[q] == 0) continue;
+        const int m = d(i1, q);
+        for (int n2 = 0; n2 < p && q + n2 < Q1; ++n2) {
+          if (T.co[q * p + n2] < 0) continue;
+          const int cw = d(i1 + 1, q + n2);
+          z* out = T.th + T.thoff[q] + T.co[q * p + n2];
+          int ld2;
+          const long o2 = s2.blk(q, n2, p, d, i1 + 1, &ld2);
+          if (m == 0 || s1.lmat[q] < 0 || o2 < 0) {
+            gt.push_back(gtask(out, T.C[q], T.R[q], cw, 0, 0));  // zero block
+            continue;
+          }
+          const int s0 = int(gs.size());
+          gs.push_back(gseg(cs[i]->site(i1) + s1.lmat[q], m, cs[i]->site(i1 + 1) + o2, ld2, m, 0));
+          gt.push_back(gtask(out, T.C[q], T.R[q], cw, s0, 1));
+        }
+      }
+    }
+    gemm(gt, gs);
+  }
+  void apply_gate(std::vector<Chain*>& cs, std::vector<ThetaJob>& th, int i1, const std::vector<double>& uf,
+                  const std::vector<double>& ut, const std::vector<double>& tau, const std::vector<int>& fwd,
+                  int mode, bool lonely) {
+    std::vector<GateChain> gc(cs.size());
+    std::vector<GateTask> tasks;
+    std::vector<int> flat;
+    std::vector<size_t> base(cs.size());
+    long long tot = 0;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const ThetaJob& T = th[i];
+      base[i] = flat.size();
+      flat.resize(flat.size() + size_t(Q1) * (2 + 2 * p), -1);
+      int* tb = flat.data() + base[i];
+      for (int q = 0; q < Q1; ++q) {
+        if (T.thoff[q] > (1L << 30)) throw Error(2, "Θ too large for 32-bit offsets");
+        tb[q] = int(T.thoff[q]);
+        tb[Q1 + q] = T.C[q];
+      }
+      for (int x = 0; x < Q1 * p; ++x) { tb[2 * Q1 + x] = T.ro[x]; tb[2 * Q1 + Q1 * p + x] = T.co[x]; }
+      const Dims& d = cs[i]->dims;
+      for (int ql = 0; ql < Q1; ++ql) {
+        const int nl = d(i1 - 1, ql);
+        if (nl == 0) continue;
+        for (int D = 0; D <= 2 * (p - 1) && ql + D < Q1; ++D) {
+          const int nr = d(i1 + 1, ql + D);
+          if (nr == 0) continue;
+          GateTask t{};
+          t.chain = int(i);
+          t.ql = ql;
+          t.qr = ql + D;
+          t.nl = nl;
+          t.nr = nr;
+          t.e0 = tot;
+          tot += (long long)nl * nr;
+          tasks.push_back(t);
+        }
+      }
+    }
+    if (tasks.empty()) return;
+    const int* dflat = upload(flat);
+    for (size_t i = 0; i < cs.size(); ++i) {
+      GateChain& G = gc[i];
+      G.th = th[i].th;
+      G.tab = dflat + base[i];
+      G.uf = uf[i];
+      G.ut = ut[i];
+      G.tau = tau[i];
+      G.fwd = fwd[i];
+      G.mode = mode;
+      G.lonely = lonely ? 1 : 0;
+    }
+    const GateChain* dgc = upload(gc);
+    const GateTask* dt_ = upload(tasks);
+    const long long blocks = std::min<long long>((tot + NT - 1) / NT, 8192);
+    hipLaunchKernelGGL(k_gate, dim3(unsigned(blocks)), dim3(NT), 0, st, dt_, int(tasks.size()), tot, dgc, gcst,
+                       d_gf.p, d_gb.p);
+    HCK(hipGetLastError());
+  }
+
+  // two-site decomposition of Θ into sites i1, i1+1 (denmatDecomp +
+  // write-back + normalisation of the centre, :173-199 / :206-213)
+  void two_site(std::vector<Chain*>& cs, std::vector<ThetaJob>& th, int i1, int dir) {
+    std::vector<DecompJob> jobs(cs.size());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      const ThetaJob& T = th[i];
+      QMat& M = jobs[i].M;
+      M.R = T.R;
+      M.C = T.C;
+      M.segs.assign(Q1, {});
+      const Dims& d = cs[i]->dims;
+      for (int q = 0; q < Q1; ++q) {
+        if (T.R[q] == 0 || T.C[q] == 0) continue;
+        // column segments n2 (for Y's write-back into site i1+1 blocks)
+        for (int n2 = 0; n2 < p && q + n2 < Q1; ++n2) {
+          if (T.co[q * p + n2] < 0) continue;
+          const int w = d(i1 + 1, q + n2);
+          M.segs[q].push_back(Seg{T.th + T.thoff[q] + T.co[q * p + n2], T.C[q], T.co[q * p + n2], w});
+        }
+      }
+      jobs[i].dir = dir;
+      jobs[i].cutoff = cutoff;
+      jobs[i].maxm = maxm;
+      jobs[i].normalize = 1;
+      jobs[i].bound = bound_row(i1, false);
+    }
+    EigRun R;
+    decompose_eig(jobs, R);
+    std::vector<std::vector<z*>> xdst(cs.size(), std::vector<z*>(Q1, nullptr));
+    std::vector<std::vector<std::vector<z*>>> ydst(cs.size(), std::vector<std::vector<z*>>(Q1));
+    std::vector<Dims> nd(cs.size());
+    for (size_t i = 0; i < cs.size(); ++i) {
+      nd[i] = cs[i]->dims;
+      for (int q = 0; q < Q1; ++q) nd[i].at(i1, q) = jobs[i].kept[q];
+      SiteLayout s1 = site_layout(nd[i], i1, p), s2 = site_layout(nd[i], i1 + 1, p);
+      for (int q = 0; q < Q1; ++q) {
+        if (jobs[i].kept[q] <= 0) continue;
+        if (s1.lmat[q] >= 0) xdst[i][q] = cs[i]->other(i1) + s1.lmat[q];
+        for (int n2 = 0; n2 < p && q + n2 < Q1; ++n2) {
+          if (th[i].co[q * p + n2] < 0) continue;
+          int ld;
+          const long o = s2.blk(q, n2, p, nd[i], i1 + 1, &ld);
+          if (o < 0) throw Error(4, "internal: two-site write-back block missing");
+          ydst[i][q].push_back(cs[i]->other(i1 + 1) + o);
+        }
+      }
+    }
+    decompose_factors(jobs, R, xdst, ydst);
+    for (size_t i = 0; i < cs.size(); ++i) {
+      cs[i]->dims = nd[i];
+      cs[i]->flip(i1);
+      cs[i]->flip(i1 + 1);
+    }
+  }
+
+  // ------------------------------------------------------------ load / store
+  void copy_sites(const View& src, const std::vector<z*>& dst, std::vector<CTask>& ct) {
+    for (int k = 1; k <= L; ++k) {
+      const long n = site_layout(*src.d, k, p).size;
+      if (n <= 0) continue;
+      // one row of n elements (k_copy tasks are 2-D; split long rows)
+      const int W = 1 << 20;
+      for (long o = 0; o < n; o += W) {
+        const int w = int(std::min<long>(W, n - o));
+        ct.push_back(ctask(src.site[k] + o, dst[k] + o, 1, w, w, w));
+      }
+    }
+  }
+  void load(Chain* c, const View& s) {
+    c->dims = *s.d;
+    std::fill(c->cur.begin(), c->cur.end(), 0);
+    std::vector<CTask> ct;
+    copy_sites(s, c->buf[0], ct);
+    copy(ct);
+  }
+  void store(State& s, const Chain* c) {
+    s.dims = c->dims;
+    set_state_layout(s);
+    std::vector<z*> dst(L + 1, nullptr);
+    for (int k = 1; k <= L; ++k) dst[k] = s.data + s.off[k];
+    std::vector<CTask> ct;
+    copy_sites(c->view(), dst, ct);
+    copy(ct);
+  }
+  void load_many(std::vector<Chain*>& cs, const std::vector<View>& vs) {
+    std::vector<CTask> ct;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      cs[i]->dims = *vs[i].d;
+      std::fill(cs[i]->cur.begin(), cs[i]->cur.end(), 0);
+      copy_sites(vs[i], cs[i]->buf[0], ct);
+    }
+    copy(ct);
+  }
+  void store_many(const std::vector<State*>& ss, const std::vector<Chain*>& cs) {
+    std::vector<CTask> ct;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      ss[i]->dims = cs[i]->dims;
+      set_state_layout(*ss[i]);
+      std::vector<z*> dst(L + 1, nullptr);
+      for (int k = 1; k <= L; ++k) dst[k] = ss[i]->data + ss[i]->off[k];
+      copy_sites(cs[i]->view(), dst, ct);
+    }
+    copy(ct);
+  }
+
+  // host interchange format (blocks (q, n) in (q, n) order) <-> device layout
+  void upload_state(State& s, const int* dims, const double* data) {
+    s.dims.L = L;
+    s.dims.Q1 = Q1;
+    s.dims.v.assign(dims, dims + size_t(L + 1) * Q1);
+    int wid = 0;
+    for (int b = 0; b <= L; ++b) wid = std::max(wid, s.dims.bond(b));
+    set_caps(wid);
+    set_state_layout(s);
+    std::vector<z> buf(static_cast<size_t>(state_cap));
+    size_t off = 0;
+    for (int k = 1; k <= L; ++k) {
+      SiteLayout sl = site_layout(s.dims, k, p);
+      for (int q = 0; q < Q1; ++q)
+        for (int n = 0; n < p && q + n < Q1; ++n) {
+          const size_t cnt = size_t(s.dims(k - 1, q)) * s.dims(k, q + n);
+          if (cnt == 0) continue;
+          int ld;
+          const long o = sl.blk(q, n, p, s.dims, k, &ld);
+          for (size_t e = 0; e < cnt; ++e) buf[s.off[k] + o + e] = mk(data[2 * (off + e)], data[2 * (off + e) + 1]);
+          off += cnt;
+        }
+    }
+    HCK(hipMemcpyAsync(s.data, buf.data(), sizeof(z) * state_cap, hipMemcpyHostToDevice, st));
+    sync();
+  }
+  size_t download_view(const View& v, int* dims, double* data, size_t cap) {
+    const Dims& d = *v.d;
+    size_t tot = 0;
+    for (int k = 1; k <= L; ++k)
+      for (int q = 0; q < Q1; ++q)
+        for (int n = 0; n < p && q + n < Q1; ++n) tot += size_t(d(k - 1, q)) * d(k, q + n);
+    if (tot > cap) return tot;
+    std::memcpy(dims, d.v.data(), sizeof(int) * d.v.size());
+    size_t off = 0;
+    for (int k = 1; k <= L; ++k) {
+      SiteLayout sl = site_layout(d, k, p);
+      std::vector<z> h(std::max<long>(sl.size, 1));
+      if (sl.size > 0) HCK(hipMemcpyAsync(h.data(), v.site[k], sizeof(z) * sl.size, hipMemcpyDeviceToHost, st));
+      sync();
+      for (int q = 0; q < Q1; ++q)
+        for (int n = 0; n < p && q + n < Q1; ++n) {
+          const size_t cnt = size_t(d(k - 1, q)) * d(k, q + n);
+          if (cnt == 0) continue;
+          int ld;
+          const long o = sl.blk(q, n, p, d, k, &ld);
+          for (size_t e = 0; e < cnt; ++e) {
+            data[2 * (off + e)] = h[o + e].x;
+            data[2 * (off + e) + 1] = h[o + e].y;
+          }
+          off += cnt;
+        }
+    }
+    return tot;
+  }
+
+  // ------------------------------------------------------------ dH application
+  // exactApplyMPO(propDeriv, psi) (src/OptimalControl.cpp:256, :302), as the
+  // oracle restates it: bond-doubled exact MPO x MPS, gauge moves right with
+  // the 1e-14 cutoff, then a right-to-left sweep truncating with the
+  // stepper's Cutoff/Maxm.  Result right-orthonormal, centre site 1,
+  // unnormalised; written into the normal chains `out`.
+  void apply_dH(const std::vector<View>& in, std::vector<Chain*>& out) {
+    const size_t B = in.size();
+    reserve_chains(std::max<int>(nchain_cap_w, int(B)), true);
+    std::vector<Chain*> w(B);
+    for (size_t i = 0; i < B; ++i) w[i] = acquire(true);
+    std::vector<CTask> ct;
+    for (size_t i = 0; i < B; ++i) {
+      const Dims& d = *in[i].d;
+      Dims& f = w[i]->dims;
+      f = d;
+      for (int b = 1; b < L; ++b)
+        for (int q = 0; q < Q1; ++q) f.at(b, q) = 2 * d(b, q);
+      std::fill(w[i]->cur.begin(), w[i]->cur.end(), 0);
+      for (int k = 1; k <= L; ++k) {
+        SiteLayout sf = site_layout(f, k, p), sd = site_layout(d, k, p);
+        if (sf.size > 0) {
+          // zero fill, then the three placements of every block
+          const int W = 1 << 20;
+          for (long o = 0; o < sf.size; o += W) {
+            const int wd = int(std::min<long>(W, sf.size - o));
+            ct.push_back(ctask(nullptr, w[i]->site(k) + o, 1, wd, 0, wd, 2));
+          }
+        }
+      }
+    }
+    copy(ct);
+    for (size_t i = 0; i < B; ++i) {
+      const Dims& d = *in[i].d;
+      const Dims& f = w[i]->dims;
+      for (int k = 1; k <= L; ++k) {
+        SiteLayout sf = site_layout(f, k, p), sd = site_layout(d, k, p);
+        for (int q = 0; q < Q1; ++q)
+          for (int n = 0; n < p && q + n < Q1; ++n) {
+            int lds, ldf;
+            const long os = sd.blk(q, n, p, d, k, &lds), of = sf.blk(q, n, p, f, k, &ldf);
+            if (os < 0 || of < 0) continue;
+            const int dl = d(k - 1, q), dr = d(k, q + n);
+            const bool lb = k == 1, rb = k == L;
+            auto put = [&](int s, int t, double fac) {
+              if (lb && s == 1) return;
+              if (rb && t == 0) return;
+              const int ro = lb ? 0 : s * dl, co = rb ? 0 : t * dr;
+              CTask c = ctask(in[i].site[k] + os, w[i]->site(k) + of + long(ro) * ldf + co, dl, dr, lds, ldf);
+              c.f = mk(fac, 0);
+              ct.push_back(c);
+            };
+            put(0, 0, 1.0);
+            if (dH[n] != 0.0) put(0, 1, dH[n]);
+            put(1, 1, 1.0);
+          }
+      }
+    }
+    copy(ct);
+    for (int k = 1; k < L; ++k) { move_right(w, k, kGaugeCutoff, kNoMaxm, true); sync(); }
+    for (int k = L; k > 1; --k) { move_left(w, k, cutoff, maxm, false); sync(); }
+    for (size_t i = 0; i < B; ++i) load(out[i], w[i]->view());
+    sync();
+    for (auto* c : w) release(c);
+  }
+
+  // ------------------------------------------------------------ overlaps
+  // <x|y> (conj on x; overlapC) or <x| sum_k dH_k |y> per pair, batched:
+  // transfer matrices E_k[q'] = sum_n X(q,n)^H (E_{k-1}[q] Y(q,n)), q' = q+n
+  std::vector<std::complex<double>> overlaps(const std::vector<View>& xs, const std::vector<View>& ys, bool with_dH) {
+    const size_t B = xs.size();
+    std::vector<std::complex<double>> res(B, 0.0);
+    if (B == 0) return res;
+    // environments: E0 (nothing applied), E1 (dH applied once) per pair and sector
+    struct Env {
+      std::vector<z*> e0, e1;
+    };
+    std::vector<Env> cur(B), nxt(B);
+    // workspace: environments of two consecutive bonds + T products
+    size_t need = 0;
+    for (size_t i = 0; i < B; ++i)
+      for (int b = 0; b <= L; ++b) {
+        size_t s = 0;
+        for (int q = 0; q < Q1; ++q) s += size_t((*xs[i].d)(b, q)) * (*ys[i].d)(b, q);
+        need = std::max(need, s);
+      }
+    // bond 0: E0 = [[1]] in sector 0, E1 = 0
+    std::vector<CTask> ct;
+    for (size_t i = 0; i < B; ++i) {
+      cur[i].e0.assign(Q1, nullptr);
+      cur[i].e1.assign(Q1, nullptr);
+      z* one = walloc<z>(2);
+      CTask c = ctask(nullptr, one, 1, 1, 0, 1, 8);  // fill with f = 1
+      ct.push_back(c);
+      cur[i].e0[0] = one;
+      if (with_dH) {
+        ct.push_back(ctask(nullptr, one + 1, 1, 1, 0, 1, 2));
+        cur[i].e1[0] = one + 1;
+      }
+    }
+    copy(ct);
+    for (int k = 1; k <= L; ++k) {
+      std::vector<GTask> gt;
+      std::vector<GSeg> gs;
+      // T0/T1[q][n] = E[q] Y(q, n)
+      struct TT {
+        std::vector<z*> t0, t1;
+      };
+      std::vector<TT> tt(B);
+      for (size_t i = 0; i < B; ++i) {
+        const Dims& dx = *xs[i].d;
+        const Dims& dy = *ys[i].d;
+        SiteLayout sy = site_layout(dy, k, p);
+        tt[i].t0.assign(size_t(Q1) * p, nullptr);
+        tt[i].t1.assign(size_t(Q1) * p, nullptr);
+        for (int q = 0; q < Q1; ++q) {
+          const int rx = dx(k - 1, q), ry = dy(k - 1, q);
+          if (rx == 0 || ry == 0 || !cur[i].e0[q]) continue;
+          for (int n = 0; n < p && q + n < Q1; ++n) {
+            int ldy;
+            const long oy = sy.blk(q, n, p, dy, k, &ldy);
+            if (oy < 0 || dx(k, q + n) == 0) continue;
+            z* t0 = walloc<z>(size_t(rx) * ldy);
+            int s0 = int(gs.size());
+            gs.push_back(gseg(cur[i].e0[q], ry, ys[i].site[k] + oy, ldy, ry, 0));
+            gt.push_back(gtask(t0, ldy, rx, ldy, s0, 1));
+            tt[i].t0[q * p + n] = t0;
+            if (with_dH) {
+              z* t1 = walloc<z>(size_t(rx) * ldy);
+              s0 = int(gs.size());
+              gs.push_back(gseg(cur[i].e1[q], ry, ys[i].site[k] + oy, ldy, ry, 0));
+              gt.push_back(gtask(t1, ldy, rx, ldy, s0, 1));
+              tt[i].t1[q * p + n] = t1;
+            }
+          }
+        }
+      }
+      gemm(gt, gs);
+      // E'[q'] = sum_n X(q'-n, n)^H T[q'-n][n]  (E1' also + dH[n] X^H T0)
+      for (size_t i = 0; i < B; ++i) {
+        const Dims& dx = *xs[i].d;
+        const Dims& dy = *ys[i].d;
+        SiteLayout sx = site_layout(dx, k, p);
+        nxt[i].e0.assign(Q1, nullptr);
+        nxt[i].e1.assign(Q1, nullptr);
+        for (int qq = 0; qq < Q1; ++qq) {
+          const int cx = dx(k, qq), cy = dy(k, qq);
+          if (cx == 0 || cy == 0) continue;
+          const int s0 = int(gs.size());
+          int ns = 0;
+          std::vector<GSeg> s1;
+          for (int n = 0; n < p && qq - n >= 0; ++n) {
+            const int q = qq - n;
+            const z* t0 = tt[i].t0[q * p + n];
+            if (!t0) continue;
+            int ldx;
+            const long ox = sx.blk(q, n, p, dx, k, &ldx);
+            if (ox < 0) continue;
+            const int rx = dx(k - 1, q);
+            gs.push_back(gseg(xs[i].site[k] + ox, ldx, t0, cy, rx, 1));
+            ++ns;
+            if (with_dH) {
+              s1.push_back(gseg(xs[i].site[k] + ox, ldx, tt[i].t1[q * p + n], cy, rx, 1));
+              if (dH[n] != 0.0) s1.push_back(gseg(xs[i].site[k] + ox, ldx, t0, cy, rx, 1, dH[n]));
+            }
+          }
+          if (ns == 0) continue;
+          z* e0 = walloc<z>(size_t(cx) * cy);
+          gt.push_back(gtask(e0, cy, cx, cy, s0, ns));
+          nxt[i].e0[qq] = e0;
+          if (with_dH) {
+            z* e1 = walloc<z>(size_t(cx) * cy);
+            const int s1b = int(gs.size());
+            gs.insert(gs.end(), s1.begin(), s1.end());
+            gt.push_back(gtask(e1, cy, cx, cy, s1b, int(s1.size())));
+            nxt[i].e1[qq] = e1;
+          }
+        }
+      }
+      gemm(gt, gs);
+      std::swap(cur, nxt);
+    }
+    std::vector<z> h(B, mk(0, 0));
+    for (size_t i = 0; i < B; ++i) {
+      const z* e = with_dH ? cur[i].e1[Q] : cur[i].e0[Q];
+      if (e) HCK(hipMemcpyAsync(&h[i], e, sizeof(z), hipMemcpyDeviceToHost, st));
+    }
+    sync();
+    for (size_t i = 0; i < B; ++i) res[i] = std::complex<double>(h[i].x, h[i].y);
+    return res;
+  }
+};
+
+}  // namespace hbm
+
+// =====================================================================
+// Entry points used by ocmps.hip (the C-ABI) — see hbm.hpp
+// =====================================================================
+using hbm::Chain;
+using hbm::State;
+using hbm::View;
+
+struct hbm_engine {
+  std::unique_ptr<hbm::Engine> E;
+  std::string err;
+  int N = 0;
+  bool have_states = false, have_psi = false, have_xi = false, have_xih = false;
+  // state slots: 0 init, 1 target, 2.. scratch, then psi_t, xi_t, xiH_t
+  int psi_base() const { return 4; }
+  int xi_base() const { return 4 + N; }
+  int xih_base() const { return 4 + 2 * N; }
+  double ms[8] = {0};
+  long launches[8] = {0};
+  long steps[8] = {0};
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+namespace {
+int widest_of(const hbm::Engine& E, const int* dims) {
+  int w = 0;
+  for (int b = 0; b <= E.L; ++b) {
+    int a = 0;
+    for (int q = 0; q < E.Q1; ++q) a += dims[b * E.Q1 + q];
+    w = std::max(w, a);
+  }
+  return w;
+}
+template <class F>
+int guard(hbm_engine* h, F f) {
+  try {
+    HCK(hipSetDevice(h->E->device));
+    f();
+    return 0;
+  } catch (const hbm::Error& e) {
+    h->err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    h->err = e.what();
+    return 3;
+  }
+}
+struct Timer {
+  hbm_engine* h;
+  int kind;
+  Timer(hbm_engine* h_, int k) : h(h_), kind(k) { HCK(hipEventRecord(h->e0, h->E->st)); }
+  void stop(long nsteps = 0) {
+    HCK(hipEventRecord(h->e1, h->E->st));
+    HCK(hipEventSynchronize(h->e1));
+    float ms = 0;
+    HCK(hipEventElapsedTime(&ms, h->e0, h->e1));
+    h->ms[kind] += ms;
+    h->launches[kind] += 1;
+    h->steps[kind] += nsteps;
+  }
+};
+}  // namespace
+
+int hbm_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm,
+               const std::vector<int>& md, const std::vector<int>& mdz, const std::vector<double>& gf,
+               const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal,
+               const std::vector<int>& gates, hbm_engine** out, std::string& err) {
+  auto* h = new hbm_engine;
+  h->E.reset(new hbm::Engine(device, L, p, npart, J, tstep, cutoff, maxm));
+  try {
+    HCK(hipSetDevice(device));
+    h->E->init(md, mdz, gf, gb, glo, gsz, goff, gtotal, gates);
+    HCK(hipEventCreate(&h->e0));
+    HCK(hipEventCreate(&h->e1));
+  } catch (const hbm::Error& e) {
+    err = e.what();
+    delete h;
+    return e.code;
+  }
+  *out = h;
+  return 0;
+}
+void hbm_destroy(hbm_engine* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->E->device);
+  if (h->e0) (void)hipEventDestroy(h->e0);
+  if (h->e1) (void)hipEventDestroy(h->e1);
+  delete h;
+}
+const char* hbm_last_error(const hbm_engine* h) { return h->err.c_str(); }
+size_t hbm_mps_max_nelem(const hbm_engine* h) { return h->E->mps_max_nelem(); }
+
+int hbm_set_tstep(hbm_engine* h, double tstep, const std::vector<double>& gf, const std::vector<double>& gb,
+                  const int* glo, const int* gsz, const int* goff, int gtotal) {
+  return guard(h, [&] {
+    h->E->dt = tstep;
+    h->E->set_gates(gf, gb, glo, gsz, goff, gtotal);
+    h->have_psi = h->have_xi = h->have_xih = false;
+  });
+}
+
+int hbm_steps(hbm_engine* h, int n, const int* dims, const double* const* data, const double* u, int u_stride,
+              int nsteps, const int* fwd, int* out_dims, double* const* out_data, const size_t* out_cap,
+              size_t* out_nelem) {
+  return guard(h, [&] {
+    hbm::Engine& E = *h->E;
+    const int nsq = (E.L + 1) * E.Q1;
+    for (int i = 0; i < n; ++i) E.set_caps(widest_of(E, dims + size_t(i) * nsq));
+    E.reserve_states(size_t(h->xih_base() + h->N + n));
+    const int sb = h->xih_base() + h->N;
+    for (int i = 0; i < n; ++i) E.upload_state(E.states[sb + i], dims + size_t(i) * nsq, data[i]);
+    E.reserve_chains(std::max(E.nchain_cap, n), false);
+    std::vector<Chain*> cs(n);
+    std::vector<View> vs(n);
+    for (int i = 0; i < n; ++i) { cs[i] = E.acquire(false); vs[i] = E.states[sb + i].view(); }
+    E.load_many(cs, vs);
+    Timer t(h, 4);
+    std::vector<double> uf(n), ut(n);
+    std::vector<int> fw(fwd, fwd + n);
+    for (int s = 0; s < nsteps; ++s) {
+      for (int i = 0; i < n; ++i) { uf[i] = u[size_t(i) * u_stride + s]; ut[i] = u[size_t(i) * u_stride + s + 1]; }
+      E.step(cs, uf, ut, fw);
+    }
+    t.stop(long(n) * nsteps);
+    for (int i = 0; i < n; ++i) {
+      const size_t tot = E.download_view(cs[i]->view(), out_dims + size_t(i) * nsq, out_data[i], out_cap[i]);
+      if (out_nelem) out_nelem[i] = tot;
+      if (tot > out_cap[i]) { for (auto* c : cs) E.release(c); throw hbm::Error(2, "output buffer too small"); }
+    }
+    for (auto* c : cs) E.release(c);
+  });
+}
+
+int hbm_overlap(hbm_engine* h, const int* dx, const double* x, const int* dy, const double* y, int with_dH,
+                double* out) {
+  return guard(h, [&] {
+    hbm::Engine& E = *h->E;
+    E.set_caps(std::max(widest_of(E, dx), widest_of(E, dy)));
+    E.reserve_states(size_t(h->xih_base() + h->N + 2));
+    const int sb = h->xih_base() + h->N;
+    E.upload_state(E.states[sb], dx, x);
+    E.upload_state(E.states[sb + 1], dy, y);
+    Timer t(h, 1);
+    auto r = E.overlaps({E.states[sb].view()}, {E.states[sb + 1].view()}, with_dH != 0);
+    t.stop();
+    out[0] = r[0].real();
+    out[1] = r[0].imag();
+  });
+}
+
+int hbm_apply_dH(hbm_engine* h, const int* dims, const double* data, int* out_dims, double* out_data, size_t cap,
+                 size_t* nelem, double* norm) {
+  return guard(h, [&] {
+    hbm::Engine& E = *h->E;
+    E.set_caps(widest_of(E, dims));
+    E.reserve_states(size_t(h->xih_base() + h->N + 1));
+    const int sb = h->xih_base() + h->N;
+    E.upload_state(E.states[sb], dims, data);
+    E.reserve_chains(std::max(E.nchain_cap, 1), false);
+    std::vector<Chain*> cs{E.acquire(false)};
+    Timer t(h, 2);
+    E.apply_dH({E.states[sb].view()}, cs);
+    t.stop();
+    const double n2 = E.site_norm2({cs[0]->view()}, 1)[0];
+    if (norm) *norm = std::sqrt(std::max(0.0, n2));
+    const size_t tot = E.download_view(cs[0]->view(), out_dims, out_data, cap);
+    if (nelem) *nelem = tot;
+    E.release(cs[0]);
+    if (tot > cap) throw hbm::Error(2, "output buffer too small");
+  });
+}
+
+int hbm_set_states(hbm_engine* h, const int* dt_, const double* t, const int* di, const double* in) {
+  return guard(h, [&] {
+    hbm::Engine& E = *h->E;
+    int wid = 0;
+    for (int b = 0; b <= E.L; ++b) {
+      int a = 0, c = 0;
+      for (int q = 0; q < E.Q1; ++q) { a += dt_[b * E.Q1 + q]; c += di[b * E.Q1 + q]; }
+      wid = std::max(wid, std::max(a, c));
+    }
+    E.set_caps(wid);  // before any slot exists: inputs may be wider than Maxm
+    E.reserve_states(size_t(h->xih_base() + h->N + 1));
+    E.upload_state(E.states[1], dt_, t);
+    E.upload_state(E.states[0], di, in);
+    h->have_states = true;
+    h->have_psi = h->have_xi = h->have_xih = false;
+  });
+}
+
+static void hbm_prepare_N(hbm_engine* h, int N) {
+  if (N != h->N) {
+    h->N = N;
+    h->have_psi = h->have_xi = h->have_xih = false;
+  }
+  h->E->reserve_states(size_t(h->xih_base() + N + 2));
+}
+
+int hbm_propagate(hbm_engine* h, const double* u, int N, int which) {
+  return guard(h, [&] {
+    if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
+    hbm_prepare_N(h, N);
+    hbm::Engine& E = *h->E;
+    E.reserve_chains(std::max(E.nchain_cap, 2), false);
+    std::vector<Chain*> cs;
+    std::vector<int> kind;  // 0 psi, 1 xi
+    if (which & 1) { cs.push_back(E.acquire(false)); kind.push_back(0); }
+    if (which & 2) { cs.push_back(E.acquire(false)); kind.push_back(1); }
+    std::vector<View> vs;
+    for (int k : kind) vs.push_back(E.states[k == 0 ? 0 : 1].view());
+    E.load_many(cs, vs);
+    std::vector<State*> ss;
+    for (int k : kind) ss.push_back(&E.states[k == 0 ? h->psi_base() : h->xi_base() + N - 1]);
+    E.store_many(ss, cs);
+    Timer t(h, 0);
+    std::vector<double> uf(cs.size()), ut(cs.size());
+    std::vector<int> fw(cs.size());
+    for (int s = 0; s + 1 < N; ++s) {
+      for (size_t i = 0; i < cs.size(); ++i) {
+        if (kind[i] == 0) { uf[i] = u[s]; ut[i] = u[s + 1]; fw[i] = 1; }
+        else { uf[i] = u[N - 1 - s]; ut[i] = u[N - 2 - s]; fw[i] = 0; }
+      }
+      E.step(cs, uf, ut, fw);
+      ss.clear();
+      for (size_t i = 0; i < cs.size(); ++i)
+        ss.push_back(&E.states[kind[i] == 0 ? h->psi_base() + s + 1 : h->xi_base() + N - 2 - s]);
+      E.store_many(ss, cs);
+    }
+    E.sync();
+    t.stop(long(cs.size()) * (N - 1));
+    for (auto* c : cs) E.release(c);
+    if (which & 1) { h->have_psi = true; }
+    if (which & 2) { h->have_xi = true; h->have_xih = false; }
+  });
+}
+
+static std::vector<std::complex<double>> hbm_pairs(hbm_engine* h, const std::vector<int>& xs,
+                                                   const std::vector<int>& ys, bool dH) {
+  hbm::Engine& E = *h->E;
+  std::vector<View> vx, vy;
+  for (int s : xs) vx.push_back(E.states[s].view());
+  for (int s : ys) vy.push_back(E.states[s].view());
+  Timer t(h, 1);
+  auto r = E.overlaps(vx, vy, dH);
+  t.stop();
+  return r;
+}
+
+int hbm_overlap_factor(hbm_engine* h, double* F) {
+  return guard(h, [&] {
+    if (!h->have_psi) throw hbm::Error(4, "psi_t not propagated");
+    auto r = hbm_pairs(h, {h->psi_base() + h->N - 1}, {1}, false);
+    F[0] = r[0].real();
+    F[1] = r[0].imag();
+  });
+}
+int hbm_fidelities(hbm_engine* h, double* fid) {
+  return guard(h, [&] {
+    if (!h->have_psi) throw hbm::Error(4, "psi_t not propagated");
+    std::vector<int> xs(h->N, 1), ys(h->N);
+    for (int i = 0; i < h->N; ++i) ys[i] = h->psi_base() + i;
+    auto r = hbm_pairs(h, xs, ys, false);
+    for (int i = 0; i < h->N; ++i) fid[i] = std::norm(r[i]);
+  });
+}
+int hbm_div_t(hbm_engine* h, double* divT) {
+  return guard(h, [&] {
+    if (!h->have_psi || !h->have_xi) throw hbm::Error(4, "psi_t and xi_t must be propagated");
+    std::vector<int> xs(h->N), ys(h->N);
+    for (int i = 0; i < h->N; ++i) { xs[i] = h->xi_base() + i; ys[i] = h->psi_base() + i; }
+    auto r = hbm_pairs(h, xs, ys, true);
+    for (int i = 0; i < h->N; ++i) { divT[2 * i] = r[i].real(); divT[2 * i + 1] = r[i].imag(); }
+  });
+}
+
+// rows per batch of the Hessian / chunk of dH applications: bounded by memory
+static int hbm_batch(hbm_engine* h, int want) {
+  hbm::Engine& E = *h->E;
+  const double per = 16.0 * E.chain_elems(false) * 4.0;  // chain + its share of workspace
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  const double budget = 0.5 * double(fr);
+  int b = int(std::max(1.0, std::min(double(want), budget / std::max(per, 1.0))));
+  return std::min(b, 1024);
+}
+
+int hbm_xi_dH(hbm_engine* h) {
+  return guard(h, [&] {
+    if (!h->have_xi) throw hbm::Error(4, "xi_t not propagated");
+    hbm::Engine& E = *h->E;
+    const int N = h->N;
+    const int B = hbm_batch(h, N);
+    E.reserve_chains(std::max(E.nchain_cap, B), false);
+    Timer t(h, 2);
+    for (int t0 = 0; t0 < N; t0 += B) {
+      const int nb = std::min(B, N - t0);
+      std::vector<View> in;
+      std::vector<Chain*> out;
+      std::vector<State*> ss;
+      for (int i = 0; i < nb; ++i) {
+        in.push_back(E.states[h->xi_base() + t0 + i].view());
+        out.push_back(E.acquire(false));
+        ss.push_back(&E.states[h->xih_base() + t0 + i]);
+      }
+      E.apply_dH(in, out);
+      E.store_many(ss, out);
+      E.sync();
+      for (auto* c : out) E.release(c);
+    }
+    t.stop();
+    h->have_xih = true;
+  });
+}
+
+// calcHessianRow (src/OptimalControl.cpp:251-279) for a set of rows, in
+// batches: psiH_i = dH psi_i, then all rows of a batch step in lockstep
+// (row i's s-th step uses u[i+s-1] -> u[i+s]) and overlap with xiH_{i+s}
+int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int nrows, const double* F,
+                     const double* divT, double* H) {
+  return guard(h, [&] {
+    if (N != h->N || !h->have_psi || !h->have_xih) throw hbm::Error(4, "propagate(3) + xi_dH first");
+    hbm::Engine& E = *h->E;
+    const std::complex<double> Fc(F[0], F[1]);
+    auto dv = [&](int i) { return std::complex<double>(divT[2 * i], divT[2 * i + 1]); };
+    const double dt2 = E.dt * E.dt;
+    std::vector<int> rs(rows, rows + nrows);
+    std::sort(rs.begin(), rs.end());
+    const int B = hbm_batch(h, nrows);
+    E.reserve_chains(std::max(E.nchain_cap, B), false);
+    Timer t(h, 3);
+    long nsteps = 0;
+    for (int r0 = 0; r0 < nrows; r0 += B) {
+      const int nb = std::min(B, nrows - r0);
+      std::vector<int> ri(rs.begin() + r0, rs.begin() + r0 + nb);
+      std::vector<Chain*> cs(nb);
+      std::vector<View> in(nb);
+      for (int k = 0; k < nb; ++k) { cs[k] = E.acquire(false); in[k] = E.states[h->psi_base() + ri[k]].view(); }
+      E.apply_dH(in, cs);
+      std::vector<View> vs;
+      for (auto* c : cs) vs.push_back(c->view());
+      const std::vector<double> n2 = E.site_norm2(vs, 1);
+      std::vector<double> nrm(nb);
+      for (int k = 0; k < nb; ++k) nrm[k] = std::sqrt(std::max(0.0, n2[k]));
+      // diagonal (:259-264)
+      {
+        std::vector<View> xs;
+        for (int k = 0; k < nb; ++k) xs.push_back(E.states[h->xih_base() + ri[k]].view());
+        auto ov = E.overlaps(xs, vs, false);
+        for (int k = 0; k < nb; ++k) {
+          const int i = ri[k];
+          const double v1 = (Fc * ov[k]).real(), v2 = -std::norm(dv(i));
+          H[size_t(i) * N + i] = dt2 * (v1 + v2);
+        }
+      }
+      // off-diagonal (:266-278): lockstep over s
+      std::vector<int> act(nb);
+      for (int k = 0; k < nb; ++k) act[k] = k;
+      for (int s = 1;; ++s) {
+        std::vector<Chain*> a;
+        std::vector<int> ak;
+        for (int k : act)
+          if (ri[k] + s <= N - 2) { a.push_back(cs[k]); ak.push_back(k); }
+        if (a.empty()) break;
+        std::vector<double> uf(a.size()), ut(a.size());
+        std::vector<int> fw(a.size(), 1);
+        for (size_t m = 0; m < a.size(); ++m) { const int j = ri[ak[m]] + s; uf[m] = u[j - 1]; ut[m] = u[j]; }
+        E.step(a, uf, ut, fw);
+        nsteps += long(a.size());
+        std::vector<View> xs, ys;
+        for (size_t m = 0; m < a.size(); ++m) {
+          xs.push_back(E.states[h->xih_base() + ri[ak[m]] + s].view());
+          ys.push_back(a[m]->view());
+        }
+        auto ov = E.overlaps(xs, ys, false);
+        for (size_t m = 0; m < a.size(); ++m) {
+          const int k = ak[m], i = ri[k], j = i + s;
+          const double v1 = (Fc * ov[m] * nrm[k]).real();
+          const double v2 = -(dv(i) * std::conj(dv(j))).real();
+          const double r = dt2 * (v1 + v2);
+          H[size_t(i) * N + j] = r;
+          H[size_t(j) * N + i] = r;
+        }
+        act = ak;
+      }
+      for (auto* c : cs) E.release(c);
+    }
+    t.stop(nsteps);
+  });
+}
+
+int hbm_get_state(hbm_engine* h, int which, int t, int* dims, double* data, size_t cap, size_t* nelem) {
+  return guard(h, [&] {
+    if (t < 0 || t >= h->N) throw hbm::Error(1, "t out of range");
+    const bool ok = (which == 0 && h->have_psi) || (which == 1 && h->have_xi) || (which == 2 && h->have_xih);
+    if (!ok) throw hbm::Error(4, "requested trajectory not available");
+    const int base = which == 0 ? h->psi_base() : (which == 1 ? h->xi_base() : h->xih_base());
+    const size_t tot = h->E->download_view(h->E->states[base + t].view(), dims, data, cap);
+    if (nelem) *nelem = tot;
+    if (tot > cap) throw hbm::Error(2, "output buffer too small");
+  });
+}
+
+int hbm_stats(hbm_engine* h, int kind, double* ms, long* launches, double* bytes, double* flops, long* steps) {
+  if (kind == 7) {  // the GEMM (MFMA contraction) kernel: HIP-event time, algorithmic flops / bytes
+    (void)guard(h, [&] { h->E->sync(); });
+    if (ms) *ms = h->E->gemm_ms;
+    if (launches) *launches = h->E->gemm_launches;
+    if (bytes) *bytes = h->E->gemm_bytes;
+    if (flops) *flops = h->E->gemm_flops;
+    if (steps) *steps = 0;
+    return 0;
+  }
+  if (ms) *ms = h->ms[kind];
+  if (launches) *launches = h->launches[kind];
+  if (bytes) *bytes = 0;
+  if (flops) *flops = 0;
+  if (steps) *steps = h->steps[kind];
+  return 0;
+}
+void hbm_reset_stats(hbm_engine* h) {
+  for (int k = 0; k < 8; ++k) { h->ms[k] = 0; h->launches[k] = 0; h->steps[k] = 0; }
+  (void)guard(h, [&] { h->E->sync(); });
+  h->E->gemm_ms = h->E->gemm_flops = h->E->gemm_bytes = 0;
+  h->E->gemm_launches = 0;
+}
+int hbm_info_L(const hbm_engine* h) { return h->E->L; }
+bool hbm_have(const hbm_engine* h, int what) {
+  switch (what) {
+    case 0: return h->have_states;
+    case 1: return h->have_psi;
+    case 2: return h->have_xi;
+    case 3: return h->have_xih;
+  }
+  return false;
+}
+int hbm_N(const hbm_engine* h) { return h->N; }

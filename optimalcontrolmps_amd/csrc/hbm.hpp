@@ -1,0 +1,45 @@
+// Host interface between the C-ABI (ocmps.hip) and the HBM-resident engine
+// (hbm.hip).  Same argument meaning and return codes as the ocg_* entry
+// points of include/ocmps.h they back; an ocg_ctx whose configuration does
+// not fit the LDS chain engine (or that asked for this engine) forwards here.
+#pragma once
+
+#include <cstddef>
+#include <string>
+#include <vector>
+
+struct hbm_engine;
+
+int hbm_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm,
+               const std::vector<int>& md, const std::vector<int>& mdz, const std::vector<double>& gf,
+               const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal,
+               const std::vector<int>& gates, hbm_engine** out, std::string& err);
+void hbm_destroy(hbm_engine* h);
+const char* hbm_last_error(const hbm_engine* h);
+size_t hbm_mps_max_nelem(const hbm_engine* h);
+int hbm_set_tstep(hbm_engine* h, double tstep, const std::vector<double>& gf, const std::vector<double>& gb,
+                  const int* glo, const int* gsz, const int* goff, int gtotal);
+// n states (dims[i], data[i]) take nsteps steps each, controls u[i*u_stride + s]
+int hbm_steps(hbm_engine* h, int n, const int* dims, const double* const* data, const double* u, int u_stride,
+              int nsteps, const int* fwd, int* out_dims, double* const* out_data, const size_t* out_cap,
+              size_t* out_nelem);
+int hbm_overlap(hbm_engine* h, const int* dx, const double* x, const int* dy, const double* y, int with_dH,
+                double* out);
+int hbm_apply_dH(hbm_engine* h, const int* dims, const double* data, int* out_dims, double* out_data, size_t cap,
+                 size_t* nelem, double* norm);
+int hbm_set_states(hbm_engine* h, const int* dims_target, const double* target, const int* dims_init,
+                   const double* init);
+int hbm_propagate(hbm_engine* h, const double* u, int N, int which);
+int hbm_overlap_factor(hbm_engine* h, double* F);
+int hbm_fidelities(hbm_engine* h, double* fid);
+int hbm_div_t(hbm_engine* h, double* divT);
+int hbm_xi_dH(hbm_engine* h);
+int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int nrows, const double* F,
+                     const double* divT, double* H);
+int hbm_get_state(hbm_engine* h, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
+// kinds 0-6 as ocg_kernel_stats (HIP-event phase times); 7: the MFMA GEMM
+// kernel (k_gemm) with its algorithmic bytes and flops
+int hbm_stats(hbm_engine* h, int kind, double* ms, long* launches, double* bytes, double* flops, long* steps);
+void hbm_reset_stats(hbm_engine* h);
+bool hbm_have(const hbm_engine* h, int what);  // 0 states, 1 psi, 2 xi, 3 xiH
+int hbm_N(const hbm_engine* h);

@@ -149,23 +149,36 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
 //   k_row_overlaps  one workgroup per stored psiH_i(j): overlap with xiH_j, H_ij
 // Producers and consumers live in one grid; consumers only ever wait on
 // blocks 0 and 1, which are dispatched first, so progress does not depend on
-// co-residency.  A watchdog (~2^24 polls, ~15 s) aborts waits and flags err.
-__device__ __forceinline__ void publish_flag(int* flag, int epoch) {
+// co-residency.  Every publication also bumps a progress counter
+// (flags[2N]); a waiter gives up (err |= OCG_ERR_WATCHDOG) only after ~2^24
+// polls (~15 s) during which no producer published anything, so a slow but
+// live pipeline (long horizons, large chains, several shards per GPU) never
+// trips it.
+__device__ __forceinline__ void publish_flag(int* flag, int epoch, int* progress) {
   __threadfence();
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(progress, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 template <int NT>
-__device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, int* err) {
+__device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, int* err, const int* progress) {
   if (threadIdx.x == 0) {
     int ok = 1;
     long spins = 0;
+    int seen = __hip_atomic_load(progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // relaxed polls (no L2 invalidate per poll), one acquire fence on success
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
       __builtin_amdgcn_s_sleep(32);  // ~2k cycles between polls: a waiting row is idle, not a poller
+      const int now = __hip_atomic_load(progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (now != seen) {
+        seen = now;
+        spins = 0;
+      }
       if (++spins > (1L << 24) || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = 0;
-        atomicOr(err, 2);
+        atomicOr(err, OCG_ERR_WATCHDOG);
         break;
       }
     }
@@ -187,6 +200,7 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
   Chain<NT> c(P, smem);
   c.load_tables(gf, gb, md);
   const int b = blockIdx.x;
+  int* const progress = flags + 2 * N;
   double bytes = 0, flops = 0, nsteps = 0;
   if (b < 2) {
     // calcPsi / calcXi (src/OptimalControl.cpp:375-407), every state published
@@ -197,12 +211,12 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     c.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
     int t = fwd ? 0 : N - 1;
     c.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
-    publish_flag(fl + t, epoch);
+    publish_flag(fl + t, epoch, progress);
     for (int s = 0; s + 1 < N; ++s) {
       const int tn = fwd ? t + 1 : t - 1;
       c.step(u[t], u[tn], fwd, s + 2 == N);  // closing gauge move on the last step only (Chain::step)
       c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
-      publish_flag(fl + tn, epoch);
+      publish_flag(fl + tn, epoch, progress);
       t = tn;
     }
     nsteps = N - 1;
@@ -211,7 +225,7 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     // take t = N-1-w, N-1-w-nxw, ... in the order the xi chain publishes
     // them, so few workgroups keep up with it and every row keeps a CU
     for (int t = N - 1 - (b - 2); t >= 0; t -= nxw) {
-      if (!await_flag(c, flags + N + t, epoch, err)) return;
+      if (!await_flag(c, flags + N + t, epoch, err, progress)) return;
       c.load(SLOT_D(pool, P, xi_base + t), SLOT_X(pool, P, xi_base + t));
       c.apply_dH();
       c.store(SLOT_D(pool, P, xih_base + t), SLOT_X(pool, P, xih_base + t));
@@ -220,7 +234,7 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     const int r = b - 2 - nxw;
     if (r >= nrows) return;
     const int i = rows[r];
-    if (!await_flag(c, flags + i, epoch, err)) return;
+    if (!await_flag(c, flags + i, epoch, err, progress)) return;
     // psiH = exactApplyMPO(propDeriv, psi_t[i]); normiH = norm(psiH) (:256-257)
     c.load(SLOT_D(pool, P, psi_base + i), SLOT_X(pool, P, psi_base + i));
     c.apply_dH();

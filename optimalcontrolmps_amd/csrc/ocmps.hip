@@ -19,6 +19,7 @@
 
 #include "../../include/ocmps.h"
 #include "engine.hpp"
+#include "hbm.hpp"
 #include "engine_device.hpp"
 #include "params.hpp"
 
@@ -120,6 +121,7 @@ struct KStat {
 
 struct ocg_ctx {
   int device = 0;
+  hbm_engine* hbm = nullptr;  // set: this context runs on the HBM-resident engine (hbm.hip)
   OcgParams P{};
   int lds_np = 0;   // LDS of the kernels that never step (no plan slots)
   int lds_ovl = 0;  // LDS of the overlap-only kernels (compact layout)
@@ -331,6 +333,22 @@ static int begin_kernel(ocg_ctx* c) {
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   return 0;
 }
+// After a synchronised launch: a nonzero device error word (a Jacobi that hit
+// its sweep cap, a pipeline watchdog) fails the call with OCG_ENUM and
+// invalidates every device-resident trajectory (a partly rewritten slot must
+// not be read as a valid psi_t / xi_t / xiH_t).
+static int check_err(ocg_ctx* c) {
+  int err = 0;
+  HIPCHK(c, hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (!err) return 0;
+  HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
+  c->have_psi = c->have_xi = c->have_xih = false;
+  std::string m;
+  if (err & OCG_ERR_JACOBI) m += "eigensolver did not converge within its sweep cap; ";
+  if (err & OCG_ERR_WATCHDOG) m += "pipeline watchdog: a consumer saw no producer progress for ~15 s; ";
+  return fail(c, OCG_ENUM, m.empty() ? std::string("kernel error flag set") : m);
+}
+
 static int end_kernel(ocg_ctx* c, int kind) {
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
@@ -339,7 +357,7 @@ static int end_kernel(ocg_ctx* c, int kind) {
   HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->kst[kind].ms += ms;
   c->kst[kind].launches += 1;
-  return 0;
+  return check_err(c);
 }
 
 static int set_lds(ocg_ctx* c) {
@@ -396,6 +414,12 @@ static int finish_params(ocg_ctx* c) {
   return 0;
 }
 
+
+// forward an HBM-engine status (its message becomes the context's)
+static int hb(ocg_ctx* c, int rc) {
+  if (rc) c->err = hbm_last_error(c->hbm);
+  return rc;
+}
 extern "C" {
 
 const char* ocg_last_error(const ocg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
@@ -421,19 +445,43 @@ int ocg_device_count(int* n) {
   return OCG_OK;
 }
 
-int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm, ocg_ctx** out) {
+// the HBM-resident engine for configurations beyond the LDS chain engine
+static int create_hbm(ocg_ctx* c, int L, int p, int npart, double tstep, double cutoff, int maxm) {
+  std::vector<int> md, mdz;
+  ocg_host::rank_bounds(L, p, npart, md, mdz);
+  OcgParams G{};
+  G.p = p;
+  G.dt = tstep;
+  std::vector<double> gf, gb;
+  ocg_host::gate_tables(G, c->J, gf, gb);
+  std::string err;
+  const int rc = hbm_create(c->device, L, p, npart, c->J, tstep, cutoff, maxm, md, mdz, gf, gb, G.glo, G.gsz,
+                            G.goff, G.gtotal, ocg_host::gate_order(L), &c->hbm, err);
+  if (rc) return fail(c, rc, "HBM engine: " + err);
+  c->P.L = L; c->P.p = p; c->P.Q = npart; c->P.Q1 = npart + 1; c->P.nsq = (L + 1) * (npart + 1);
+  c->P.dt = tstep; c->P.cutoff = cutoff; c->P.maxm = maxm > 0 ? maxm : 5000;
+  return 0;
+}
+
+int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm, int engine,
+                  ocg_ctx** out) {
   if (!out) { g_create_error = "out is NULL"; return OCG_EINVAL; }
   *out = nullptr;
+  if (engine < 0 || engine > 2) { g_create_error = "engine must be 0 (auto), 1 (LDS) or 2 (HBM)"; return OCG_EINVAL; }
   auto* c = new ocg_ctx;
   c->device = device;
   c->J = J;
-  int rc = build_params(c, L, p, npart, tstep, cutoff, maxm);
   auto bail = [&](int code) {
     g_create_error = c->err;
     ocg_destroy(c);
     return code;
   };
-  if (rc) return bail(rc);
+  if (L < 2 || L > OCG_MAXL || p < 2 || p > OCG_MAXP || npart < 0 || npart + 1 > OCG_MAXQ1 ||
+      npart > L * (p - 1) || !(tstep == tstep) || !(cutoff >= 0)) {
+    int rc = build_params(c, L, p, npart, tstep, cutoff, maxm);  // same messages as before
+    if (!rc) { c->err = "bad argument"; rc = OCG_EINVAL; }
+    return bail(rc);
+  }
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0) {
@@ -442,15 +490,37 @@ int ocg_create(int device, int L, int p, int npart, double J, double tstep, doub
   }
   if (device < 0 || device >= ndev) { c->err = "device index out of range"; return bail(OCG_EINVAL); }
   if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(OCG_EHIP); }
-  // gate tables first: their size (gtotal) is part of the LDS layout
-  if ((rc = upload_gates(c))) return bail(rc);
-  if ((rc = finish_params(c))) return bail(rc);
+  int rc = 0;
+  if (engine != 2) {
+    rc = build_params(c, L, p, npart, tstep, cutoff, maxm);
+    // gate tables first: their size (gtotal) is part of the LDS layout
+    if (!rc) rc = upload_gates(c);
+    if (!rc) rc = finish_params(c);
+    if (rc == OCG_ECAP && engine == 0) {
+      // beyond the single-workgroup LDS engine: the HBM-resident engine
+      const std::string why = c->err;
+      ocg_ctx* h = new ocg_ctx;
+      h->device = device;
+      h->J = J;
+      std::swap(c, h);
+      ocg_destroy(h);
+      if ((rc = create_hbm(c, L, p, npart, tstep, cutoff, maxm))) return bail(rc);
+    } else if (rc) {
+      return bail(rc);
+    }
+  } else if ((rc = create_hbm(c, L, p, npart, tstep, cutoff, maxm))) {
+    return bail(rc);
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->evh[0]) != hipSuccess || hipEventCreate(&c->evh[1]) != hipSuccess ||
       hipEventCreate(&c->evh[2]) != hipSuccess || hipEventCreate(&c->evh[3]) != hipSuccess) {
     c->err = "stream/event creation failed";
     return bail(OCG_EHIP);
+  }
+  if (c->hbm) {
+    *out = c;
+    return 0;
   }
   if (hipMalloc(&c->d_md, sizeof(int) * c->md.size()) != hipSuccess ||
       hipMemcpy(c->d_md, c->md.data(), sizeof(int) * c->md.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -460,15 +530,21 @@ int ocg_create(int device, int L, int p, int npart, double J, double tstep, doub
     c->err = "device allocation failed";
     return bail(OCG_EHIP);
   }
+  c->P.err = c->d_err;
   if ((rc = set_lds(c))) return bail(rc);
   if ((rc = ensure_slots(c, 8))) return bail(rc);
   *out = c;
   return 0;
 }
 
+int ocg_create(int device, int L, int p, int npart, double J, double tstep, double cutoff, int maxm, ocg_ctx** out) {
+  return ocg_create_ex(device, L, p, npart, J, tstep, cutoff, maxm, 0, out);
+}
+
 int ocg_destroy(ocg_ctx* c) {
   if (!c) return 0;
   if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->hbm) hbm_destroy(c->hbm);
   if (c->d_gf) (void)hipFree(c->d_gf);
   if (c->d_gb) (void)hipFree(c->d_gb);
   if (c->d_md) (void)hipFree(c->d_md);
@@ -500,6 +576,14 @@ int ocg_destroy(ocg_ctx* c) {
 
 int ocg_get_info(const ocg_ctx* c, ocg_info* info) {
   if (!c || !info) return OCG_EINVAL;
+  if (c->hbm) {
+    info->L = c->P.L; info->p = c->P.p; info->Q = c->P.Q;
+    info->mps_max_nelem = hbm_mps_max_nelem(c->hbm);
+    info->lds_bytes = 0;
+    info->block_threads = 256;
+    info->device = c->device;
+    return 0;
+  }
   info->L = c->P.L; info->p = c->P.p; info->Q = c->P.Q;
   info->mps_max_nelem = size_t(c->P.cap);
   info->lds_bytes = c->P.lds_bytes;
@@ -513,6 +597,14 @@ int ocg_set_tstep(ocg_ctx* c, double tstep) {
   HIPCHK(c, hipSetDevice(c->device));
   c->P.dt = tstep;
   c->have_psi = c->have_xi = c->have_xih = false;
+  if (c->hbm) {
+    OcgParams G{};
+    G.p = c->P.p;
+    G.dt = tstep;
+    std::vector<double> gf, gb;
+    ocg_host::gate_tables(G, c->J, gf, gb);
+    return hb(c, hbm_set_tstep(c->hbm, tstep, gf, gb, G.glo, G.gsz, G.goff, G.gtotal));
+  }
   return upload_gates(c);
 }
 
@@ -531,6 +623,11 @@ static int launch_steps(ocg_ctx* c, int slot, const double* u, int nsteps, int f
 int ocg_steps(ocg_ctx* c, const int* dims, const double* data, const double* u, int nsteps, int forward,
               int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem) {
   if (!c || !dims || !data || !u || nsteps < 0) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (c->hbm) {
+    const int fw = forward;
+    double* od[1] = {out_data};
+    return hb(c, hbm_steps(c->hbm, 1, dims, &data, u, nsteps + 1, nsteps, &fw, out_dims, od, &out_cap, out_nelem));
+  }
   HIPCHK(c, hipSetDevice(c->device));
   int slot = c->slot_tmp(0);
   if (int rc = upload_mps(c, slot, dims, data)) return rc;
@@ -543,6 +640,46 @@ int ocg_step(ocg_ctx* c, const int* dims, const double* data, double from, doubl
              double* out_data, size_t out_cap, size_t* out_nelem) {
   double u[2] = {from, to};
   return ocg_steps(c, dims, data, u, 1, forward, out_dims, out_data, out_cap, out_nelem);
+}
+
+int ocg_step_batch(ocg_ctx* c, int n, const int* dims, const double* const* data, const double* u_from,
+                   const double* u_to, int forward, int* out_dims, double* const* out_data, const size_t* out_cap,
+                   size_t* out_nelem) {
+  if (!c || n < 0 || (n > 0 && (!dims || !data || !u_from || !u_to || !out_dims || !out_data || !out_cap)))
+    return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (n == 0) return 0;
+  if (c->hbm) {
+    std::vector<double> uu(2 * size_t(n));
+    std::vector<int> fw(n, forward);
+    for (int i = 0; i < n; ++i) { uu[2 * i] = u_from[i]; uu[2 * i + 1] = u_to[i]; }
+    return hb(c, hbm_steps(c->hbm, n, dims, data, uu.data(), 2, 1, fw.data(), out_dims, out_data, out_cap, out_nelem));
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  const OcgParams& P = c->P;
+  // scratch slots after the trajectory slots (their contents are left alone)
+  const int base = 6 + 4 * c->N;
+  if (int rc = ensure_slots(c, base + n)) return rc;
+  std::vector<int> slots(n);
+  std::vector<double> uu(2 * size_t(n));
+  for (int i = 0; i < n; ++i) {
+    slots[i] = base + i;
+    if (int rc = upload_mps(c, slots[i], dims + size_t(i) * P.nsq, data[i])) return rc;
+    uu[2 * i] = u_from[i];
+    uu[2 * i + 1] = u_to[i];
+  }
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, 2 * n)) return rc;
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, n)) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_u, uu.data(), sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, slots.data(), sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_steps, dim3(n), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx, n, c->d_u, 2, 1, forward, c->d_stats + 4 * 3);
+  if (int rc = end_kernel(c, 4)) return rc;
+  for (int i = 0; i < n; ++i)
+    if (int rc = download_mps(c, slots[i], out_dims + size_t(i) * P.nsq, out_data[i], out_cap[i],
+                              out_nelem ? out_nelem + i : nullptr))
+      return rc;
+  return 0;
 }
 
 static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::vector<int>& ys, int with_dH,
@@ -568,6 +705,7 @@ static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::ve
 int ocg_overlap(ocg_ctx* c, const int* dims_x, const double* x, const int* dims_y, const double* y, int with_dH,
                 double* out) {
   if (!c || !dims_x || !x || !dims_y || !y || !out) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_overlap(c->hbm, dims_x, x, dims_y, y, with_dH, out));
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = upload_mps(c, c->slot_tmp(0), dims_x, x)) return rc;
   if (int rc = upload_mps(c, c->slot_tmp(1), dims_y, y)) return rc;
@@ -599,6 +737,7 @@ static int launch_apply_dH(ocg_ctx* c, const std::vector<int>& in, const std::ve
 int ocg_apply_dH(ocg_ctx* c, const int* dims, const double* data, int* out_dims, double* out_data, size_t out_cap,
                  size_t* out_nelem, double* norm) {
   if (!c || !dims || !data) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_apply_dH(c->hbm, dims, data, out_dims, out_data, out_cap, out_nelem, norm));
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = upload_mps(c, c->slot_tmp(0), dims, data)) return rc;
   double nrm = 0;
@@ -610,6 +749,7 @@ int ocg_apply_dH(ocg_ctx* c, const int* dims, const double* data, int* out_dims,
 int ocg_set_states(ocg_ctx* c, const int* dims_target, const double* target, const int* dims_init,
                    const double* init) {
   if (!c || !dims_target || !target || !dims_init || !init) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_set_states(c->hbm, dims_target, target, dims_init, init));
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = upload_mps(c, c->slot_target(), dims_target, target)) return rc;
   if (int rc = upload_mps(c, c->slot_init(), dims_init, init)) return rc;
@@ -620,6 +760,7 @@ int ocg_set_states(ocg_ctx* c, const int* dims_target, const double* target, con
 
 int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
   if (!c || !u || N < 2 || which < 1 || which > 3) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_propagate(c->hbm, u, N, which));
   if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
   HIPCHK(c, hipSetDevice(c->device));
   const OcgParams& P = c->P;
@@ -643,6 +784,7 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
 
 int ocg_overlap_factor(ocg_ctx* c, double* F) {
   if (!c || !F) return OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_overlap_factor(c->hbm, F));
   if (!c->have_psi) return fail(c, OCG_ESTATE, "psi_t not propagated");
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<zc> r;
@@ -655,6 +797,7 @@ int ocg_overlap_factor(ocg_ctx* c, double* F) {
 
 int ocg_fidelities(ocg_ctx* c, double* fid) {
   if (!c || !fid) return OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_fidelities(c->hbm, fid));
   if (!c->have_psi) return fail(c, OCG_ESTATE, "psi_t not propagated");
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<int> xs(c->N, c->slot_target()), ys(c->N);
@@ -667,6 +810,7 @@ int ocg_fidelities(ocg_ctx* c, double* fid) {
 
 int ocg_div_t(ocg_ctx* c, double* divT) {
   if (!c || !divT) return OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_div_t(c->hbm, divT));
   if (!c->have_psi || !c->have_xi) return fail(c, OCG_ESTATE, "psi_t and xi_t must be propagated");
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<int> xs(c->N), ys(c->N);
@@ -679,6 +823,7 @@ int ocg_div_t(ocg_ctx* c, double* divT) {
 
 int ocg_xi_dH(ocg_ctx* c) {
   if (!c) return OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_xi_dH(c->hbm));
   if (!c->have_xi) return fail(c, OCG_ESTATE, "xi_t not propagated");
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<int> in(c->N), outs(c->N);
@@ -691,6 +836,11 @@ int ocg_xi_dH(ocg_ctx* c) {
 int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, const double* F,
                      const double* divT, double* H) {
   if (!c || !u || !rows || !F || !divT || !H || nrows < 0) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  if (c->hbm) {
+    for (int r = 0; r < nrows; ++r)
+      if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
+    return hb(c, hbm_hessian_rows(c->hbm, u, N, rows, nrows, F, divT, H));
+  }
   if (N != c->N || !c->have_psi || !c->have_xih) return fail(c, OCG_ESTATE, "propagate(3) + xi_dH first");
   for (int r = 0; r < nrows; ++r)
     if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
@@ -748,10 +898,26 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
   return 0;
 }
 
+// getHessian's fidelity part from the separate entry points (calcPsiXiDivT,
+// xiHlist, calcHessianRow over all rows: src/OptimalControl.cpp:281-338)
+static int hessian_unfused(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                           double* F) {
+  if (int rc = ocg_propagate(c, u, N, 3)) return rc;
+  if (int rc = ocg_div_t(c, divT)) return rc;
+  if (int rc = ocg_overlap_factor(c, F)) return rc;
+  if (int rc = ocg_xi_dH(c)) return rc;
+  return ocg_hessian_rows(c, u, N, rows, nrows, F, divT, H);
+}
+
 int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                 double* F) {
   if (!c || !u || !H || !divT || !F || (nrows > 0 && !rows) || nrows < 0 || N < 4)
     return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (c->hbm) {
+    for (int r = 0; r < nrows; ++r)
+      if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
+    return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
+  }
   if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
   for (int r = 0; r < nrows; ++r)
     if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
@@ -766,17 +932,30 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   if (int rc = ensure_buf(c, c->d_pc, c->pc_cap, N + 1)) return rc;
   if (int rc = ensure_buf(c, c->d_rows, c->rows_cap, 2 * nrows + 2)) return rc;
   if (int rc = ensure_buf(c, c->d_prn, c->prn_cap, nrows + 1)) return rc;
-  if (2 * N > c->flags_cap) {  // publication flags start at 0 (< any epoch)
+  if (2 * N + 1 > c->flags_cap) {  // publication flags (+ progress counter) start at 0 (< any epoch)
     if (c->d_flags) (void)hipFree(c->d_flags);
     c->d_flags = nullptr;
     c->flags_cap = 0;
-    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N)) return rc;
+    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N + 1)) return rc;
     HIPCHK(c, hipMemset(c->d_flags, 0, sizeof(int) * c->flags_cap));
     c->epoch = 0;
   }
-  // stored row states: row i keeps psiH_i(j), j = i..N-2
-  std::vector<int> rb(2 * nrows + 1);  // rows[0..nrows) then rbase[0..nrows]
+  // stored row states: row i keeps psiH_i(j), j = i..N-2 (O(N^2) states).
+  // Past the memory budget (or int offsets) the unfused path runs instead:
+  // same arithmetic per row (test_fused_equals_unfused_bitwise), O(N) states.
   size_t total = 0;
+  for (int r = 0; r < nrows; ++r) total += size_t(N - 1 - rows[r]);
+  {
+    static const double budget_mb = [] {
+      const char* e = std::getenv("OCG_RS_BUDGET_MB");
+      return e ? std::atof(e) : 16384.0;
+    }();
+    const double need = double(total) * (sizeof(zc) * double(P.cap) + sizeof(int) * double(P.nsq));
+    if (total > size_t(INT32_MAX / 2) || need > budget_mb * 1048576.0)
+      return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
+  }
+  std::vector<int> rb(2 * nrows + 1);  // rows[0..nrows) then rbase[0..nrows]
+  total = 0;
   for (int r = 0; r < nrows; ++r) rb[r] = rows[r];
   for (int r = 0; r < nrows; ++r) {
     rb[nrows + r] = int(total);
@@ -865,7 +1044,13 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     c->kst[kinds[k]].ms += ms;
     c->kst[kinds[k]].launches += 1;
   }
-  if (err) return fail(c, OCG_ENUM, "pipeline watchdog: a consumer timed out waiting for a trajectory state");
+  if (err) {
+    c->have_psi = c->have_xi = c->have_xih = false;
+    HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
+    return fail(c, OCG_ENUM, std::string((err & OCG_ERR_WATCHDOG) ? "pipeline watchdog: a consumer saw no producer "
+                                                                    "progress for ~15 s; " : "") +
+                                 ((err & OCG_ERR_JACOBI) ? "eigensolver did not converge within its sweep cap" : ""));
+  }
   c->have_psi = c->have_xi = c->have_xih = true;
   for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
   F[0] = pc[N].x;
@@ -882,6 +1067,7 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
 
 int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t cap, size_t* nelem) {
   if (!c || !dims || !data) return OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_get_state(c->hbm, which, t, dims, data, cap, nelem));
   if (t < 0 || t >= c->N) return fail(c, OCG_EINVAL, "t out of range");
   bool ok = (which == 0 && c->have_psi) || (which == 1 && c->have_xi) || (which == 2 && c->have_xih);
   if (!ok) return fail(c, OCG_ESTATE, "requested trajectory not available");
@@ -892,7 +1078,16 @@ int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t 
 
 int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, double* alg_bytes, double* alg_flops,
                      long* sweep_steps) {
-  if (!c || kind < 0 || kind > 6) return OCG_EINVAL;
+  if (!c || kind < 0 || kind > 7) return OCG_EINVAL;
+  if (c->hbm) return hb(c, hbm_stats(c->hbm, kind, total_ms, launches, alg_bytes, alg_flops, sweep_steps));
+  if (kind == 7) {  // the MFMA contraction kernel exists only in the HBM engine
+    if (total_ms) *total_ms = 0;
+    if (launches) *launches = 0;
+    if (alg_bytes) *alg_bytes = 0;
+    if (alg_flops) *alg_flops = 0;
+    if (sweep_steps) *sweep_steps = 0;
+    return 0;
+  }
   HIPCHK(c, hipSetDevice(c->device));
   double s[3];
   HIPCHK(c, hipMemcpy(s, c->d_stats + 3 * kind, sizeof(s), hipMemcpyDeviceToHost));
@@ -923,6 +1118,10 @@ int ocg_profile(ocg_ctx* c, double* out32, int reset) {
 
 int ocg_reset_stats(ocg_ctx* c) {
   if (!c) return OCG_EINVAL;
+  if (c->hbm) {
+    hbm_reset_stats(c->hbm);
+    return 0;
+  }
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemset(c->d_stats, 0, sizeof(double) * 24));
   for (auto& k : c->kst) k = KStat{};

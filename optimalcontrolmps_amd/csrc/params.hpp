@@ -80,6 +80,30 @@ inline void gate_tables(OcgParams& P, double J, std::vector<double>& gf, std::ve
   P.gtotal = off;
 }
 
+// Per-sector Schmidt-rank bounds for the HBM engine (no LDS capacity
+// limits): md[b][q] = min(HS_left, HS_right), mdz[b][q] = min(HS_left,
+// 2 min(HS_left, HS_right)) (inside the dH zip-up), clamped to 2^30.
+inline void rank_bounds(int L, int p, int npart, std::vector<int>& md, std::vector<int>& mdz) {
+  const int Q1 = npart + 1;
+  md.assign(size_t(L + 1) * Q1, 0);
+  mdz.assign(size_t(L + 1) * Q1, 0);
+  for (int b = 0; b <= L; ++b)
+    for (int q = 0; q < Q1; ++q) {
+      const long long a = hs_count(b, p, q), r = hs_count(L - b, p, npart - q);
+      md[size_t(b) * Q1 + q] = int(std::min<long long>(std::min(a, r), 1LL << 30));
+      mdz[size_t(b) * Q1 + q] = int(std::min<long long>(std::min(a, 2 * std::min(a, r)), 1LL << 30));
+    }
+}
+
+// gate order of initJGates (src/BH_tDMRG.cpp:18-58): even bonds ascending, odd descending
+inline std::vector<int> gate_order(int L) {
+  std::vector<int> g;
+  for (int i = 1; i < L; i += 2) g.push_back(i);
+  const int offset = (L % 2 == 0) ? 2 : 1;
+  for (int i = L - offset; i >= 1; i -= 2) g.push_back(i);
+  return g;
+}
+
 // Decompositions one step performs: one per gate plus the gauge moves of
 // MPS::position between gates (the centre walk of doStep,
 // src/BH_tDMRG.cpp:173-218, as Chain::step runs it).

@@ -150,6 +150,7 @@ class GpuTDMRG::Engine {
   void setShards(size_t n) {
     if (n < 1) throw std::invalid_argument("Mininum threadCount is 1.");
     while (shards.size() > n) shards.pop_back();
+    const size_t kept = shards.size();
     int ndev = 0;
     detail::check(ocg_device_count(&ndev), nullptr, "ocg_device_count");
     while (shards.size() < n) {
@@ -161,9 +162,12 @@ class GpuTDMRG::Engine {
                     "ocg_set_states");
       shards.push_back(std::move(c));
     }
-    fresh.assign(shards.size(), 0);
-    for (size_t s = 1; s < shards.size(); ++s) fresh[s] = 1;  // shard 0 is the reference copy
-    xih_done.assign(shards.size(), 0);
+    // shards created by this call replay shard 0's controls before first use;
+    // existing shards keep their trajectories (and their flags)
+    fresh.resize(shards.size(), 1);
+    xih_done.resize(shards.size(), 0);
+    if (kept == 0) fresh[0] = 0;  // shard 0 is the reference copy
+    for (size_t s = kept; s < shards.size(); ++s) xih_done[s] = 0;
   }
   size_t nShards() const { return shards.size(); }
   // which: 1 psi_t (calcPsi), 2 xi_t (calcXi), 3 both concurrently
@@ -214,9 +218,7 @@ class GpuTDMRG::Engine {
                                      reinterpret_cast<const double*>(dT.data()), part[s].data()),
                     c, "ocg_hessian_rows");
     });
-    for (size_t s = 0; s < G; ++s)
-      for (size_t i = 0; i < N; ++i)
-        for (size_t j = 0; j < N; ++j) H[i][j] += part[s][i * N + j];
+    gather_rows(rows, part, H);
   }
   // getHessian(u, new_control = true) fidelity part in one pipelined call per
   // shard (ocg_hessian): trajectories, xiHlist and the shard's rows overlap
@@ -249,9 +251,7 @@ class GpuTDMRG::Engine {
     F = Cplx(Fv[0], Fv[1]);
     dT.resize(N);
     for (size_t i = 0; i < N; ++i) dT[i] = Cplx(dv[2 * i], dv[2 * i + 1]);
-    for (size_t s = 0; s < G; ++s)
-      for (size_t i = 0; i < N; ++i)
-        for (size_t j = 0; j < N; ++j) H[i][j] += part[s][i * N + j];
+    gather_rows(rows, part, H);
   }
   std::vector<MPS> psiTrajectory() {
     std::vector<MPS> out;
@@ -261,6 +261,18 @@ class GpuTDMRG::Engine {
   }
 
  private:
+  // Shard s wrote the entries (i, j >= i) of its rows and their mirrors; the
+  // entry sets of different shards are disjoint, so adding only those is the
+  // exact sum of the partial matrices (O(N^2) in total instead of G N^2).
+  void gather_rows(const std::vector<std::vector<int>>& rows, const std::vector<std::vector<double>>& part,
+                   rowmat& H) const {
+    for (size_t s = 0; s < rows.size(); ++s)
+      for (int i : rows[s])
+        for (size_t j = size_t(i); j + 1 < N; ++j) {
+          H[i][j] += part[s][size_t(i) * N + j];
+          if (j > size_t(i)) H[j][i] += part[s][j * N + size_t(i)];
+        }
+  }
   // bring shards created after the last propagation up to shard 0's state
   void replay_fresh() {
     for (size_t s = 0; s < shards.size(); ++s) {

@@ -167,14 +167,20 @@ class OptimalControl {
   stdvec calcFidelityGrad(const stdvec& u, const bool new_control) {
     if (new_control) {
       calculatedXi = false;
-      if (BFGS) calcPsi(u);
-      else calcPsiXiDivT(u);
-    }
-    if (BFGS) {
+      if (BFGS) {
+        // calcPsi + the inline xi propagation of the BFGS path (:210-229): xi
+        // never reads psi, so both chains run concurrently in one launch
+        engine->propagate(u, 3);
+        calcDivT();
+      } else {
+        calcPsiXiDivT(u);
+      }
+    } else if (BFGS) {
       // the reference re-propagates xi inline on every BFGS gradient (:217-229)
       engine->propagate(u, 2);
       calcDivT();
-    } else if (!calculatedXi) {
+    }
+    if (!BFGS && !calculatedXi) {
       calcXi(u);
       calcDivT();
     }

@@ -33,20 +33,41 @@ def sources():
 
 
 def build_native(force: bool = False, nt: int | None = None, verbose: bool = False) -> str:
-    """Compile csrc/ocmps.hip into the in-tree shared library (gfx950)."""
-    if not force and os.path.exists(LIB_PATH):
-        newest = max(os.path.getmtime(s) for s in sources())
-        if os.path.getmtime(LIB_PATH) >= newest:
-            return LIB_PATH
+    """Compile csrc/ocmps.hip (LDS chain engine + C-ABI) and csrc/hbm.hip (HBM
+    engine) for gfx950 into objects (in parallel) and link the in-tree shared
+    library.  Each object is rebuilt only when a source it depends on changed."""
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", LIB_PATH + ".tmp", os.path.join(CSRC, "ocmps.hip")]
+    bdir = os.path.join(PKG_DIR, "build")
+    os.makedirs(bdir, exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
     if nt:
-        cmd.insert(1, f"-DOCG_NT={int(nt)}")
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+        flags.append(f"-DOCG_NT={int(nt)}")
+    deps = {
+        "ocmps": ["ocmps.hip", "engine.hpp", "engine_device.hpp", "kernels.hpp", "params.hpp", "hbm.hpp"],
+        "hbm": ["hbm.hip", "hbm.hpp", "hbm_device.hpp"],
+    }
+    tag = f"nt{int(nt)}" if nt else "prod"
+    objs, procs = [], []
+    for name, srcs in deps.items():
+        obj = os.path.join(bdir, f"{name}.{tag}.o")
+        objs.append(obj)
+        newest = max([os.path.getmtime(os.path.join(CSRC, f)) for f in srcs] + [os.path.getmtime(HEADER)])
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < newest:
+            cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, srcs[0]), "-o", obj + ".tmp"]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append((subprocess.Popen(cmd), obj))
+    for pr, obj in procs:
+        if pr.wait() != 0:
+            raise OcgError(f"hipcc failed building {obj}")
+        os.replace(obj + ".tmp", obj)
+    if force or procs or not os.path.exists(LIB_PATH) or \
+            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(o) for o in objs):
+        cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB_PATH + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 
 
@@ -65,6 +86,8 @@ class OcgInfo(C.Structure):
 SIGNATURES = [
     ("ocg_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
                              C.POINTER(C.c_void_p)]),
+    ("ocg_create_ex", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
+                                C.c_int, C.POINTER(C.c_void_p)]),
     ("ocg_destroy", C.c_int, [C.c_void_p]),
     ("ocg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("ocg_last_error", C.c_char_p, [C.c_void_p]),
@@ -73,6 +96,8 @@ SIGNATURES = [
     ("ocg_mps_nelem", C.c_size_t, [C.c_int, C.c_int, C.c_int, ip]),
     ("ocg_step", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_steps", C.c_int, [C.c_void_p, ip, dp, dp, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_step_batch", C.c_int, [C.c_void_p, C.c_int, ip, C.POINTER(dp), dp, dp, C.c_int, ip, C.POINTER(dp), szp,
+                                 szp]),
     ("ocg_overlap", C.c_int, [C.c_void_p, ip, dp, ip, dp, C.c_int, dp]),
     ("ocg_apply_dH", C.c_int, [C.c_void_p, ip, dp, ip, dp, C.c_size_t, szp, dp]),
     ("ocg_set_states", C.c_int, [C.c_void_p, ip, dp, ip, dp]),
@@ -139,11 +164,13 @@ class Engine:
     """One device context (ocg_ctx): the BH_tDMRG stepper + device-resident
     trajectories of the OptimalControl hot path."""
 
-    def __init__(self, L, p, npart, J, tstep, cutoff, maxm=0, device=0):
+    ENGINES = {"auto": 0, "lds": 1, "hbm": 2}
+
+    def __init__(self, L, p, npart, J, tstep, cutoff, maxm=0, device=0, engine="auto"):
         self.L, self.p, self.Q = L, p, npart
         self.J, self.tstep, self.cutoff, self.maxm = J, tstep, cutoff, maxm
         h = C.c_void_p()
-        rc = lib().ocg_create(device, L, p, npart, J, tstep, cutoff, maxm, C.byref(h))
+        rc = lib().ocg_create_ex(device, L, p, npart, J, tstep, cutoff, maxm, self.ENGINES[engine], C.byref(h))
         if rc != 0:
             raise OcgError(f"ocg_create failed ({OCG_ERRORS.get(rc, rc)}): "
                            f"{lib().ocg_last_error(None).decode()}")
@@ -192,6 +219,28 @@ class Engine:
         self._chk(lib().ocg_steps(self.h, pd, pr, pu, len(uu) - 1, int(forward), fd.ctypes.data_as(ip),
                                   d.ctypes.data_as(dp), self.cap, C.byref(n)), "ocg_steps")
         return self._wrap(fd, d, n)
+
+    def step_batch(self, states, u_from, u_to, forward=True):
+        """one step of every state (own controls each) in a single launch"""
+        n = len(states)
+        if n == 0:
+            return []
+        nsq = (self.L + 1) * (self.Q + 1)
+        dims = np.ascontiguousarray(np.concatenate([m.dims for m in states]).astype(np.int32))
+        raws = [np.ascontiguousarray(m.raw()) for m in states]
+        data = (dp * n)(*[r.ctypes.data_as(dp) for r in raws])
+        uf, puf = _d(np.asarray(u_from, np.float64).reshape(n))
+        ut, put = _d(np.asarray(u_to, np.float64).reshape(n))
+        od = np.zeros(n * nsq, np.int32)
+        outs = [np.zeros(2 * self.cap) for _ in range(n)]
+        odata = (dp * n)(*[o.ctypes.data_as(dp) for o in outs])
+        caps = np.full(n, self.cap, dtype=np.uintp)
+        nel = np.zeros(n, dtype=np.uintp)
+        self._chk(lib().ocg_step_batch(self.h, n, dims.ctypes.data_as(ip), data, puf, put, int(forward),
+                                       od.ctypes.data_as(ip), odata, caps.ctypes.data_as(szp),
+                                       nel.ctypes.data_as(szp)), "ocg_step_batch")
+        return [MPS(self.L, self.p, self.Q, od[i * nsq:(i + 1) * nsq].copy(),
+                    outs[i][:2 * int(nel[i])].view(np.complex128).copy()) for i in range(n)]
 
     def overlap(self, x: MPS, y: MPS, with_dH=False) -> complex:
         out = np.zeros(2)
