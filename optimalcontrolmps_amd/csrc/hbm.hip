@@ -188,6 +188,8 @@ struct Engine {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gemm_ev;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_kept = nullptr;
+  // smallest Gram order on the register eigensolver (OCG_HBM_REGMIN overrides: A/B and tests)
+  int reg_min = kRegMin;
   double phase_ms[8] = {0};
   long phase_n[8] = {0};
   double steps_done[8] = {0};
@@ -207,6 +209,7 @@ struct Engine {
             const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal,
             const std::vector<int>& gates) {
     HCK(hipSetDevice(device));
+    if (const char* e = std::getenv("OCG_HBM_REGMIN")) reg_min = std::max(2, std::atoi(e));
     thost.pinned = true;
     HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
@@ -612,6 +615,8 @@ struct Engine {
         ++pi;
       }
       if (T > kMaxEig) throw Error(2, "decomposition with more eigenvalues than k_truncate holds");
+      // unresolved eigenvalues of every sector stay below 1e-3 cutoff total / T in sum
+      for (int i = R.job_p0[j]; i < pi; ++i) R.probs[i].thr_rel = J.cutoff > 1e-12 ? 1e-3 * J.cutoff / T : 0.0;
       maxT = std::max(maxT, T);
       TItem I{};
       I.p0 = R.job_p0[j];
@@ -633,11 +638,24 @@ struct Engine {
     const int* d_bounds = upload(bounds);
     for (auto& I : items) I.bound = d_bounds + I.p0;
     const TItem* d_items = upload(items);
-    // eigenvalues (LDS: 3 complex + 2 real vectors, plus the Gram block if small)
-    int lds_v = 64;
-    for (auto& P : R.probs) lds_v = std::max(lds_v, 64 * P.n + (P.n <= kLdsOrder ? 16 * P.n * P.n : 0) + 64);
-    hipLaunchKernelGGL(k_heev_vals, dim3(np), dim3(NT), lds_v, st, R.d_probs, np);
-    HCK(hipGetLastError());
+    // eigenvalues: blocks of order kRegMin..RNMAX on the register kernel,
+    // the rest on the LDS / L2 kernel (LDS: 3 complex + 2 real vectors, plus
+    // the Gram block if small)
+    {
+      // one launch: per block the register variant for its order (or the LDS / L2
+      // kernel), largest blocks first; dynamic LDS = max over the variants present
+      std::vector<int> order(np);
+      for (int i = 0; i < np; ++i) order[i] = i;
+      std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
+      int lds_v = 64;
+      for (int i = 0; i < np; ++i) {
+        const int n = R.probs[i].n;
+        lds_v = std::max(lds_v, (n >= reg_min && n <= RNMAX) ? reg_lds_bytes(reg_grid(n))
+                                                              : 64 * n + (n <= kLdsOrder ? 16 * n * n : 0) + 64);
+      }
+      hipLaunchKernelGGL(k_heev_vals_any, dim3(np), dim3(RNT), lds_v, st, R.d_probs, upload(order), reg_min);
+      HCK(hipGetLastError());
+    }
     int maxnp = 0;
     for (auto& I : items) maxnp = std::max(maxnp, I.np);
     hipLaunchKernelGGL(k_truncate, dim3(int(items.size())), dim3(NT), truncate_lds(maxnp), st, d_items, R.d_probs);
@@ -648,8 +666,7 @@ struct Engine {
     HCK(hipMemcpyAsync(R.h_keptw.data(), R.d_keptw, sizeof(double) * 2 * jobs.size(), hipMemcpyDeviceToHost, st));
     HCK(hipEventRecord(ev_kept, st));
     // eigenvectors of the kept eigenvalues (reads the kept counts on the device)
-    const int lds_e = 24 * maxn + 64;
-    hipLaunchKernelGGL(k_heev_vecs, dim3(np), dim3(NT), lds_e, st, R.d_probs, np);
+    hipLaunchKernelGGL(k_heev_vecs_reg, dim3(np), dim3(VNT), 0, st, R.d_probs, np);
     HCK(hipGetLastError());
     HCK(hipEventSynchronize(ev_kept));
     for (size_t j = 0; j < jobs.size(); ++j) {

@@ -287,6 +287,9 @@ struct EProb {
   z* U;
   int n, q;
   const int* kept;  // kept count of this sector (written by k_truncate)
+  // eigenvalues below thr_rel * trace may be left unresolved (k_heev_vals_reg):
+  // they are provably inside the discarded tail of the truncation (hbm_eig.hpp)
+  double thr_rel;
 };
 
 template <class T>
@@ -392,9 +395,7 @@ __device__ __forceinline__ int sturm(const double* d, const double* e2, int n, d
 
 // eigenvalues: tridiagonalise (in LDS for small orders), make the tridiagonal
 // real, bisect every eigenvalue (thread t -> the t-th largest)
-__global__ __launch_bounds__(NT) void k_heev_vals(const EProb* __restrict__ probs, int nprob) {
-  extern __shared__ __align__(16) char smem[];
-  const EProb P = probs[blockIdx.x];
+__device__ __forceinline__ void heev_vals_lds_body(const EProb& P, char* smem) {
   const int n = P.n, tid = threadIdx.x;
   if (n <= 0) return;
   __shared__ double red[NT / 64], scal[4];
@@ -693,3 +694,5 @@ __global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items
 __host__ __device__ inline int truncate_lds(int np) { return kMaxEig * (8 + 8 + 4) + 4 * (np + 2); }
 
 }  // namespace hbm
+
+#include "hbm_eig.hpp"

@@ -1,0 +1,710 @@
+// Register-resident Hermitian eigensolver of the HBM engine (Gram blocks of
+// order 64 < n <= 192: the sector blocks of chi = 256 chains).
+//
+// The reference's truncation (ITensor denmatDecomp, called at
+// src/BH_tDMRG.cpp:178,191,209) diagonalises rho = Θ Θ^H per U(1) sector.
+// k_heev_vals (hbm_device.hpp) streams the Gram block through L2 for every
+// Householder column once it outgrows LDS (n > 88): 1.5 ms per n = 194
+// block, bound by one CU's L2 bandwidth.  Here one 512-thread workgroup keeps
+// the whole lower triangle of the block in VGPRs (42 complex per lane, 168
+// VGPRs) for the n - 1 Householder steps, so the O(n^3) traffic never leaves
+// the CU; only O(n) vectors go through LDS.
+//
+// Thread grid 16 x 32: lane l of wave w is thread-row r = 2w + (l >> 5) and
+// thread-column c = l & 31; element (i, k), i >= k, lives in thread (i mod 16,
+// k mod 32), slot (a = i / 16, b = k / 32).  Slots with a < 2b hold no lower
+// element and are not stored.
+//
+// Same conventions as the L2 kernels, so either vecs kernel can follow either
+// vals kernel: Householder vector j in column j of P.A (rows j+1..n-1,
+// u[j+1] = u0), H_j = I - tau_j u u^H, subdiagonal beta_j made real by the
+// phases P.ph, eigenvalues descending in P.w.
+#pragma once
+
+namespace hbm {
+
+constexpr int RNT = 256;                 // threads of the register tridiagonalisation (1 wave per SIMD)
+constexpr int VNT = 512;                 // threads of the eigenvector kernel
+constexpr int RATMAX = 13;               // largest slot grid (k_heev_vals_reg<13>)
+constexpr int RNMAX = 16 * RATMAX;       // 208
+constexpr int kRegMin = 16;              // blocks of order >= kRegMin go to the register kernels (tiny ones: LDS kernel)
+constexpr int kRegSplit = 192;           // n <= 192: 12 x 12 slots (no spills); up to 208: 13 x 13
+// slot grid used for a block of order n (16 rows per slot)
+__host__ __device__ constexpr int reg_grid(int n) {
+  return n <= 32 ? 2 : n <= 64 ? 4 : n <= 128 ? 8 : n <= kRegSplit ? 12 : 13;
+}
+
+// Workgroup barrier that waits for LDS traffic only: __syncthreads() also
+// drains the global stores of the Householder vectors (vmcnt(0)) at every
+// barrier, which no other workgroup reads during this kernel.
+#ifdef HBM_STAMP  // diagnostic builds (tools/eig_bench): per-phase shader cycles of wave 0
+#define STAMP(slot)                                                                 \
+  do {                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    unsigned long long t_;                                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    stamp_acc[slot] += t_ - stamp_last;                                             \
+    stamp_last = t_;                                                                \
+  } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// q <- (d - x) - e2 / q with a refined hardware reciprocal (v_rcp_f64 + one
+// Newton step: relative error ~1e-18, far below the bisection tolerance)
+__device__ __forceinline__ double sturm_next(double dmx, double e2, double q) {
+  double r = __builtin_amdgcn_rcp(q);
+  r = fma(r, fma(-q, r, 1.0), r);
+  return fma(-e2, r, dmx);
+}
+// counts of eigenvalues of the real symmetric tridiagonal (d, e2) below four shifts
+__device__ __forceinline__ void sturm_count4(const double* d, const double* e2, int n, const double* x,
+                                             double pivmin, int* cnt) {
+  double q[4];
+  int c[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    q[t] = d[0] - x[t];
+    if (fabs(q[t]) < pivmin) q[t] = -pivmin;
+    c[t] = q[t] < 0 ? 1 : 0;
+  }
+  for (int i = 1; i < n; ++i) {
+    const double di = d[i], ei = e2[i - 1];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      q[t] = sturm_next(di - x[t], ei, q[t]);
+      if (fabs(q[t]) < pivmin) q[t] = -pivmin;
+      c[t] += q[t] < 0 ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) cnt[t] = c[t];
+}
+
+// All eigenvalues (descending) of a real symmetric tridiagonal held in LDS
+// (Ld, Le2 = e^2), by multisection: g = NTH / n threads per eigenvalue, each
+// evaluating four Sturm counts per round (LAPACK dstebz bounds / tolerances).
+// Work arrays in LDS: lo, hi (n), cnt (4 * NTH ints).
+template <int NTH>
+__device__ __forceinline__ void bisect_all(const double* Ld, const double* Le2, int n, double thr_rel, double* w,
+                                           double* lo, double* hi, int* cnt) {
+  const int tid = threadIdx.x;
+  __shared__ double bb[4][NTH / 64];
+  __shared__ int sres;
+  double gl = 1e300, gu = -1e300, emax = 0, tr = 0;
+  for (int i = tid; i < n; i += NTH) {
+    const double el = i > 0 ? sqrt(Le2[i - 1]) : 0.0, er = i + 1 < n ? sqrt(Le2[i]) : 0.0;
+    gl = fmin(gl, Ld[i] - el - er);
+    gu = fmax(gu, Ld[i] + el + er);
+    emax = fmax(emax, Le2[i]);
+    tr += Ld[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    gl = fmin(gl, __shfl_xor(gl, o, 64));
+    gu = fmax(gu, __shfl_xor(gu, o, 64));
+    emax = fmax(emax, __shfl_xor(emax, o, 64));
+    tr += __shfl_xor(tr, o, 64);
+  }
+  if ((tid & 63) == 0) { bb[0][tid >> 6] = gl; bb[1][tid >> 6] = gu; bb[2][tid >> 6] = emax; bb[3][tid >> 6] = tr; }
+  __syncthreads();
+  gl = bb[0][0]; gu = bb[1][0]; emax = bb[2][0]; tr = bb[3][0];
+  for (int i = 1; i < NTH / 64; ++i) {
+    gl = fmin(gl, bb[0][i]); gu = fmax(gu, bb[1][i]); emax = fmax(emax, bb[2][i]); tr += bb[3][i];
+  }
+  const double eps = 2.220446049250313e-16, safmin = 2.2250738585072014e-308;
+  const double tnorm = fmax(fabs(gl), fabs(gu));
+  const double pivmin = safmin * fmax(1.0, emax);
+  gl -= 2.0 * eps * tnorm * n + 2.0 * pivmin;
+  gu += 2.0 * eps * tnorm * n + 2.0 * pivmin;
+  const double atol = 4.0 * eps * tnorm;
+  // eigenvalues below thr are not resolved: their number from one Sturm
+  // count, each set to their mean (trace minus the resolved ones)
+  const double thr = thr_rel * tr;
+  if (tid == 0) {
+    int below = 0;
+    if (thr > 0) {
+      double x[4] = {thr, thr, thr, thr};
+      int c4[4];
+      sturm_count4(Ld, Le2, n, x, pivmin, c4);
+      below = c4[0];
+    }
+    sres = n - below;
+  }
+  __syncthreads();
+  const int nres = sres;
+  // resolved eigenvalues (the nres largest) in rounds of NTH
+  for (int t0 = 0; t0 < nres; t0 += NTH) {
+    const int ne = nres - t0 < NTH ? nres - t0 : NTH;
+    const int g = NTH / ne;  // threads per eigenvalue
+    const int t = tid / g, s = tid - t * g, te = t0 + t;
+    const int np = 4 * g + 1;  // sub-intervals per round
+    __syncthreads();
+    for (int tt = tid; tt < ne; tt += NTH) { lo[tt] = nres < n ? fmax(gl, thr) : gl; hi[tt] = gu; }
+    __syncthreads();
+    for (int it = 0; it < 128; ++it) {
+      bool active = false;
+      if (t < ne) {
+        const double l = lo[t], h = hi[t];
+        active = h - l > atol + 2.0 * eps * fmax(fabs(l), fabs(h));
+        if (active) {
+          double x[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = l + (h - l) * double(4 * s + q + 1) / np;
+          sturm_count4(Ld, Le2, n, x, pivmin, cnt + 4 * tid);
+        }
+      }
+      if (!__syncthreads_or(active)) break;
+      if (t < ne && s == 0 && active) {
+        const int idx = n - 1 - te;  // ascending index of the te-th largest
+        const double l = lo[t], h = hi[t];
+        double nl = l, nh = h;
+        for (int q = 1; q < np; ++q) {
+          const double x = l + (h - l) * double(q) / np;
+          if (cnt[4 * (t * g) + q - 1] > idx) { nh = x; break; }
+          nl = x;
+        }
+        lo[t] = nl;
+        hi[t] = nh;
+      }
+      __syncthreads();
+    }
+    for (int tt = tid; tt < ne; tt += NTH) w[t0 + tt] = 0.5 * (lo[tt] + hi[tt]);
+  }
+  if (nres < n) {
+    __syncthreads();
+    double sr = 0;
+    for (int t = tid; t < nres; t += NTH) sr += w[t];
+    for (int o = 32; o > 0; o >>= 1) sr += __shfl_xor(sr, o, 64);
+    if ((tid & 63) == 0) bb[0][tid >> 6] = sr;
+    __syncthreads();
+    sr = 0;
+    for (int i = 0; i < NTH / 64; ++i) sr += bb[0][i];
+    const double mean = fmin(fmax((tr - sr) / (n - nres), 0.0), thr);
+    for (int t = nres + tid; t < n; t += NTH) w[t] = mean;
+  }
+}
+
+// Householder tridiagonalisation with the block in registers + eigenvalues.
+// idx: the problems of this launch (blockIdx.x -> probs[idx[blockIdx.x]]).
+//
+// Thread grid 16 x 16: lane l of wave w is thread-row r = 4w + (l >> 4) and
+// thread-column c = l & 15; element (i, k), i >= k, lives in thread
+// (i mod 16, k mod 16), slot (a = i / 16, b = k / 16), b <= a: 91 complex per
+// lane (364 registers; the compiler keeps the overflow in AGPRs).
+//
+// Branch-free sweeps: the LDS vectors u, p are zero outside the trailing
+// block [j+1, n), so dead rows and columns contribute nothing to the matvec
+// and are left unchanged by the rank-2 update.  Only the diagonal slots
+// (a = b) mix lower and upper elements; their lane masks (c <= r, c < r) are
+// fixed per thread (upper elements accumulate garbage in the update and are
+// masked out of the matvec).
+__device__ __forceinline__ z zsel(bool p, z a, z b) {
+  z r;
+  r.x = p ? a.x : b.x;
+  r.y = p ? a.y : b.y;
+  return r;
+}
+// dynamic LDS of the register tridiagonalisation for slot grid RAT
+__host__ __device__ constexpr int reg_lds_bytes(int RAT) {
+  return 16 * (2 * RAT * 16 * 17 + 5 * 16 * RAT + 2) + 8 * (2 * 16 * RAT + 3 * (RNT / 64)) + 64;
+}
+template <int RAT>
+__device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
+  constexpr int RNS = RAT * (RAT + 1) / 2;  // slot (a, b), b <= a, at a (a + 1) / 2 + b
+  constexpr int NM = 16 * RAT;
+  const int n = P.n;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int r = 4 * wv + (lane >> 4), c = lane & 15;
+  // LDS (carved from the launch's dynamic buffer): row / column partials
+  // (rows padded to 17 against bank conflicts), vectors
+  typedef z Part[16][17];
+  Part* rowbuf = (Part*)smem;
+  Part* colbuf = rowbuf + RAT;
+  z(*su)[NM] = (z(*)[NM])(colbuf + RAT);
+  z* sp = (z*)(su + 2);
+  z* sbeta = sp + NM;
+  z* salpha = sbeta + NM;
+  double* sd = (double*)(salpha + 2);
+  double* se2 = sd + NM;
+  double(*sred)[RNT / 64] = (double(*)[RNT / 64])(se2 + NM);
+  double* skp = (double*)(sred + 2);
+
+  for (int i = tid; i < NM; i += RNT) {
+    su[0][i] = mk(0, 0);
+    su[1][i] = mk(0, 0);
+    sp[i] = mk(0, 0);
+  }
+  const bool dle = c <= r, dlt = c < r;  // diagonal-slot masks
+  double Ar[RNS], Ai[RNS];
+#pragma unroll
+  for (int a = 0; a < RAT; ++a)
+#pragma unroll
+    for (int b = 0; b <= a; ++b) {
+      const int s = a * (a + 1) / 2 + b;
+      const int i = 16 * a + r, k = 16 * b + c;
+      z v = mk(0, 0);
+      if (i < n && k <= i) v = P.A[(size_t)i * n + k];
+      Ar[s] = v.x;
+      Ai[s] = v.y;
+    }
+  __syncthreads();
+  // column j's owners (c = j mod 16): publish x = A[j+1.., j] (zeros at j-1,
+  // j), the partial norm over rows >= j+2 (one per wave) and the final
+  // diagonal A[j][j]
+  auto colprep = [&](int j) {
+    double sacc = 0;
+    const int bj = j >> 4;  // uniform
+    if (tid == 0 && j >= 1) su[j & 1][j - 1] = mk(0, 0);  // stale entry below the owners' rows
+    if (c == (j & 15)) {
+      z* u = su[j & 1];
+#pragma unroll
+      for (int b = 0; b < RAT; ++b) {
+        if (b != bj) continue;  // uniform
+#pragma unroll
+        for (int a = b; a < RAT; ++a) {
+          constexpr int dummy = 0;
+          (void)dummy;
+          const int s = a * (a + 1) / 2 + b;  // slot of (a, b)
+          const int i = 16 * a + r;
+          const bool live = i >= j + 1 && i < n;
+          const double xr = live ? Ar[s] : 0.0, xi = live ? Ai[s] : 0.0;
+          if (i < NM) u[i] = mk(xr, xi);
+          if (i == j) sd[j] = Ar[s];
+          if (i == j + 1) salpha[j & 1] = mk(xr, xi);
+          sacc = fma(xr, xr, fma(xi, xi, sacc));
+        }
+      }
+    }
+    sacc += __shfl_xor(sacc, 16, 64);
+    sacc += __shfl_xor(sacc, 32, 64);
+    if (lane == (j & 15)) sred[j & 1][wv] = sacc;
+  };
+#ifdef HBM_STAMP
+  unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
+#endif
+  colprep(0);
+  for (int j = 0; j + 1 < n; ++j) {
+    STAMP(0);
+    lds_barrier();  // A: column j published
+    STAMP(1);
+    z* u = su[j & 1];
+    double snorm = 0;
+#pragma unroll
+    for (int q = 0; q < RNT / 64; ++q) snorm += sred[j & 1][q];
+    const z alpha = salpha[j & 1];
+    // colprep summed |x|^2 over rows >= j+1 (alpha included): xn = ||x||,
+    // tau = 2 / (|u0|^2 + |tail|^2) = 1 / (xn (xn + |alpha|)) without cancellation
+    const double aa = sqrt(alpha.x * alpha.x + alpha.y * alpha.y), xn = sqrt(snorm);
+    double tau = 0;
+    z beta = mk(0, 0), u0 = alpha;
+    if (xn > 0) {
+      const double ia = aa > 0 ? 1.0 / aa : 0.0;
+      const z ph = aa > 0 ? mk(alpha.x * ia, alpha.y * ia) : mk(1, 0);
+      beta = mk(-ph.x * xn, -ph.y * xn);
+      u0 = mk(alpha.x + ph.x * xn, alpha.y + ph.y * xn);
+      tau = 1.0 / (xn * (xn + aa));
+    }
+    if (tid == 0) {
+      P.tau[j] = tau;
+      sbeta[j] = beta;
+      u[j + 1] = u0;  // nobody reads u[j + 1] before barrier A'
+    }
+    STAMP(2);
+    lds_barrier();  // A': u complete
+    STAMP(3);
+    // Householder vector -> column j of P.A (rows j+1 ..)
+    for (int i = j + 1 + tid; i < n; i += RNT) P.A[(size_t)i * n + j] = u[i];
+    const int a0 = (j + 1) >> 4;  // first live slot row / column (uniform)
+    if (tau != 0.0) {  // uniform: every thread computed the same reflector
+      // ---- p = tau A_t u (lower storage: row and column contributions)
+      const int aend = (n + 15) >> 4;  // slot rows holding rows < n (uniform)
+      z uk[RAT], cp[RAT];
+#pragma unroll
+      for (int b = 0; b < RAT; ++b) {
+        uk[b] = (b >= a0 && b < aend) ? u[16 * b + c] : mk(0, 0);
+        cp[b] = mk(0, 0);
+      }
+#pragma unroll
+      for (int a = 0; a < RAT; ++a) {
+        if (a < a0 || a >= aend) continue;
+        const z ui = u[16 * a + r];
+        z acc = mk(0, 0);
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+          if (b < a0) continue;
+          const int s = a * (a + 1) / 2 + b;
+          double ar = Ar[s], ai = Ai[s], cr = Ar[s], ci = Ai[s];
+          if (b == a) {
+            ar = dle ? ar : 0.0;
+            ai = dlt ? ai : 0.0;  // the diagonal is real
+            cr = dlt ? cr : 0.0;
+            ci = dlt ? ci : 0.0;
+          }
+          acc.x = fma(ar, uk[b].x, fma(-ai, uk[b].y, acc.x));
+          acc.y = fma(ar, uk[b].y, fma(ai, uk[b].x, acc.y));
+          cp[b].x = fma(cr, ui.x, fma(ci, ui.y, cp[b].x));  // conj(A) ui
+          cp[b].y = fma(cr, ui.y, fma(-ci, ui.x, cp[b].y));
+        }
+        rowbuf[a][r][c] = acc;
+      }
+#pragma unroll
+      for (int b = 0; b < RAT; ++b)
+        if (b >= a0 && b < aend) colbuf[b][r][c] = cp[b];
+      STAMP(4);
+      lds_barrier();  // B: partials in LDS
+      STAMP(5);
+      // ---- p_k for k in the trailing block, and Re(u^H p) partials
+      double kp = 0;
+      {
+        const int k = j + 1 + tid;
+        if (k < n) {
+          const int a = k >> 4, cc = k & 15;
+          z sacc = mk(0, 0);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) sacc = zadd(sacc, zadd(rowbuf[a][cc][q], colbuf[a][q][cc]));
+          const z pk = zsc(sacc, tau);
+          sp[k] = pk;
+          const z ukk = u[k];
+          kp = ukk.x * pk.x + ukk.y * pk.y;
+        }
+        if (tid == 0) sp[j] = mk(0, 0);  // leaves the trailing block
+      }
+      for (int o = 32; o > 0; o >>= 1) kp += __shfl_xor(kp, o, 64);
+      if (lane == 0) skp[wv] = kp;
+      STAMP(6);
+      lds_barrier();  // C: p and the K partials in LDS
+      STAMP(5);
+      double K = 0;
+#pragma unroll
+      for (int q = 0; q < RNT / 64; ++q) K += skp[q];
+      K *= 0.5 * tau;
+      // ---- A_t -= u w^H + w u^H, w = p - K u (zero outside the trailing block)
+#pragma unroll
+      for (int b = 0; b < RAT; ++b) {
+        const int k = 16 * b + c;
+        cp[b] = (b >= a0 && b < aend) ? zsub(sp[k], zsc(uk[b], K)) : mk(0, 0);  // cp now holds w_k
+      }
+#pragma unroll
+      for (int a = 0; a < RAT; ++a) {
+        if (a < a0 || a >= aend) continue;
+        const int i = 16 * a + r;
+        const z ui = u[i];
+        const z wi = zsub(sp[i], zsc(ui, K));
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+          if (b < a0) continue;
+          const int s = a * (a + 1) / 2 + b;
+          // v -= u_i conj(w_k) + w_i conj(u_k)
+          Ar[s] = fma(-ui.x, cp[b].x, fma(-ui.y, cp[b].y, fma(-wi.x, uk[b].x, fma(-wi.y, uk[b].y, Ar[s]))));
+          Ai[s] = fma(-ui.y, cp[b].x, fma(ui.x, cp[b].y, fma(-wi.y, uk[b].x, fma(wi.x, uk[b].y, Ai[s]))));
+        }
+      }
+    } else {
+      lds_barrier();  // keep this column's reads of sred ahead of colprep(j + 1)
+    }
+    STAMP(7);
+    colprep(j + 1);
+  }
+#ifdef HBM_STAMP
+  STAMP(0);
+  if (tid == 0)
+    for (int q = 0; q < 8; ++q) P.Z[q] = double(stamp_acc[q]);
+#endif
+  __syncthreads();
+  // ---- real tridiagonal: d (diagonal), |beta| (off-diagonal), phases
+  if (tid == 0) {
+    z dl = mk(1, 0);
+    P.ph[0] = dl;
+    for (int j = 0; j + 1 < n; ++j) {
+      const z b = sbeta[j];
+      const double ab = sqrt(b.x * b.x + b.y * b.y);
+      if (ab > 0) dl = zmul(dl, mk(b.x / ab, b.y / ab));
+      P.ph[j + 1] = dl;
+      P.e[j] = ab;
+      se2[j] = ab * ab;
+    }
+    P.e[n - 1] = 0;
+    se2[n - 1] = 0;
+  }
+  for (int j = tid; j < n; j += RNT) P.d[j] = sd[j];
+  __syncthreads();
+  // ---- eigenvalues (work arrays reuse the partial buffers)
+  double* lo = (double*)&rowbuf[0][0][0];
+  double* hi = lo + NM;
+  int* cnt = (int*)(hi + NM);
+#ifndef HBM_NO_BISECT  // timing builds of tools/eig_bench only
+  bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt);
+#endif
+}
+
+// One launch per decomposition: each workgroup picks the variant for its
+// block's order (register slot grid 2 / 4 / 8 / 12 / 13, or the LDS / L2
+// kernel for tiny and oversized blocks).  idx lists the problems, largest
+// first.  Dynamic LDS: max over the variants present.
+__global__ __launch_bounds__(RNT, 1) void k_heev_vals_any(const EProb* __restrict__ probs, const int* __restrict__ idx,
+                                                          int reg_min) {
+  extern __shared__ __align__(16) char smem_any[];
+  const EProb P = probs[idx[blockIdx.x]];
+  const int n = P.n;
+  if (n >= reg_min && n <= RNMAX) {
+    switch (reg_grid(n)) {
+      case 2: heev_vals_reg_body<2>(P, smem_any); return;
+      case 4: heev_vals_reg_body<4>(P, smem_any); return;
+      case 8: heev_vals_reg_body<8>(P, smem_any); return;
+      case 12: heev_vals_reg_body<12>(P, smem_any); return;
+      default: heev_vals_reg_body<13>(P, smem_any); return;
+    }
+  }
+  heev_vals_lds_body(P, smem_any);
+}
+
+// ------------------------------------------------------------------ vectors
+// Kept eigenvectors U = Q D Z (n x k, ld k) of one problem per workgroup.
+// Fast path (n <= RNMAX, k <= 64, Z fits LDS): inverse iteration on the real
+// tridiagonal (one lane per eigenvalue; LDL^T pivots in P.Dv), classical
+// Gram-Schmidt twice in descending order with Z in LDS, then U = D Z in
+// registers (lane = column, rows i = 8a + wave) and the reflectors applied
+// j = n-2 .. 0 from LDS blocks.  Other sizes: the same algorithm with Z and
+// U in global memory.
+constexpr int kVecLds = 110592;  // bytes of the Z / reflector-block region
+constexpr int kVecRows = (RNMAX + VNT / 64 - 1) / (VNT / 64);  // rows per thread (fast path)
+constexpr int kRefBlk = 24;                   // reflectors per LDS block
+
+template <class T>
+__device__ __forceinline__ T block_sum_r(T v, T* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < VNT / 64; ++i) s += red[i];
+  return s;
+}
+
+// inverse iteration for eigenvalue lam into column jz of Z (ld ldz), LDL^T
+// pivots in column jd of Dv (ld ldd), starting vector hashed from (i, jj)
+__device__ __forceinline__ void invit(const double* Ld, const double* Le, int n, double lam, double tiny, double* Z,
+                                      int ldz, int jz, double* Dv, int ldd, int jd, int jj) {
+  double q = Ld[0] - lam;
+  if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
+  Dv[jd] = q;
+  for (int i = 1; i < n; ++i) {
+    q = Ld[i] - lam - Le[i - 1] * Le[i - 1] / q;
+    if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
+    Dv[(size_t)i * ldd + jd] = q;
+  }
+  for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] = hrand(i, jj);
+  for (int it = 0; it < 3; ++it) {
+    double y = Z[jz], qp = Dv[jd];
+    for (int i = 1; i < n; ++i) {
+      const size_t o = (size_t)i * ldz + jz;
+      y = Z[o] - Le[i - 1] / qp * y;
+      Z[o] = y;
+      qp = Dv[(size_t)i * ldd + jd];
+    }
+    double xn = Z[(size_t)(n - 1) * ldz + jz] / Dv[(size_t)(n - 1) * ldd + jd];
+    Z[(size_t)(n - 1) * ldz + jz] = xn;
+    double ss = xn * xn;
+    for (int i = n - 2; i >= 0; --i) {
+      const size_t o = (size_t)i * ldz + jz;
+      xn = (Z[o] - Le[i] * xn) / Dv[(size_t)i * ldd + jd];
+      Z[o] = xn;
+      ss += xn * xn;
+    }
+    const double inv = ss > 0 ? 1.0 / sqrt(ss) : 0.0;
+    for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] *= inv;
+  }
+}
+constexpr int kInvBatch = 16;  // eigenvectors per inverse-iteration batch (fast path: LDS pivots)
+
+__global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__ probs, int nprob) {
+  __shared__ __align__(16) char un[kVecLds];
+  __shared__ double Lpiv[RNMAX * kInvBatch];
+  __shared__ double Ld[RNMAX], Le[RNMAX], Lc[64];
+  __shared__ z part[VNT / 64][64];
+  __shared__ double red[VNT / 64];
+  const EProb P = probs[blockIdx.x];
+  const int n = P.n, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  if (n <= 0) return;
+  const int k = *P.kept;
+  if (k <= 0) return;
+  if (n == 1) {
+    if (tid == 0) P.U[0] = mk(1, 0);
+    return;
+  }
+  const int ldz = k + 1;  // odd stride: row reads of Z by consecutive threads hit distinct banks
+  const bool fast = n <= RNMAX && k <= 64 && size_t(n) * ldz * 8 <= size_t(kVecLds);
+  double* Zl = (double*)un;
+  // generic path: the tridiagonal in global memory scratch (P.d / P.e), Z and U global
+  const double* Gd = P.d;
+  const double* Ge = P.e;
+  if (fast) {
+    for (int i = tid; i < n; i += VNT) { Ld[i] = P.d[i]; Le[i] = P.e[i]; }
+    __syncthreads();
+    Gd = Ld;
+    Ge = Le;
+  }
+  double tn = 0;
+  for (int i = tid; i < n; i += VNT) tn = fmax(tn, fabs(Gd[i]) + Ge[i] + (i > 0 ? Ge[i - 1] : 0.0));
+  for (int o = 32; o > 0; o >>= 1) tn = fmax(tn, __shfl_xor(tn, o, 64));
+  if (lane == 0) red[wv] = tn;
+  __syncthreads();
+  tn = red[0];
+  for (int q = 1; q < VNT / 64; ++q) tn = fmax(tn, red[q]);
+  __syncthreads();
+  const double tiny = 2.220446049250313e-16 * fmax(tn, 1e-300);
+  double* Z = fast ? Zl : P.Z;
+  const int lz = fast ? ldz : n;
+  if (fast) {
+    for (int jb = 0; jb < k; jb += kInvBatch) {
+      const int jj = jb + tid;
+      if (tid < kInvBatch && jj < k) invit(Ld, Le, n, P.w[jj], tiny, Zl, ldz, jj, Lpiv, kInvBatch, tid, jj);
+    }
+  } else {
+    for (int jj = tid; jj < k; jj += VNT) invit(Gd, Ge, n, P.w[jj], tiny, Z, lz, jj, P.Dv, n, jj, jj);
+  }
+  __syncthreads();
+  // classical Gram-Schmidt, twice, descending; dots split over 8 row chunks
+  double* Lcf = fast ? Lc : P.tau + n;  // generic: coefficient scratch must hold k (see decompose_eig sizing)
+  (void)Lcf;
+  for (int j = 1; j < k; ++j) {
+    for (int pass = 0; pass < 2; ++pass) {
+      // part[ch][i] = sum_{r = ch mod 8} Z[r][i] Z[r][j]
+      for (int i0 = 0; i0 < j; i0 += 64) {
+        const int i = i0 + lane;
+        double pa = 0;
+        if (i < j)
+          for (int rr = wv; rr < n; rr += VNT / 64) pa += Z[(size_t)rr * lz + i] * Z[(size_t)rr * lz + j];
+        part[wv][lane].x = pa;
+        __syncthreads();
+        if (tid < 64 && i < j) {
+          double sc = 0;
+#pragma unroll
+          for (int q = 0; q < VNT / 64; ++q) sc += part[q][tid].x;
+          part[0][tid].y = sc;
+        }
+        __syncthreads();
+        // Z[r][j] -= sum_{i in this chunk} c_i Z[r][i]
+        for (int rr = tid; rr < n; rr += VNT) {
+          double s = 0;
+          const int ie = j - i0 < 64 ? j - i0 : 64;
+          for (int q = 0; q < ie; ++q) s += part[0][q].y * Z[(size_t)rr * lz + i0 + q];
+          Z[(size_t)rr * lz + j] -= s;
+        }
+        __syncthreads();
+      }
+    }
+    double ss = 0;
+    for (int rr = tid; rr < n; rr += VNT) { const double v = Z[(size_t)rr * lz + j]; ss += v * v; }
+    ss = block_sum_r(ss, red);
+    const double inv = ss > 0 ? 1.0 / sqrt(ss) : 0.0;
+    for (int rr = tid; rr < n; rr += VNT) Z[(size_t)rr * lz + j] *= inv;
+    __syncthreads();
+  }
+  if (!fast) {
+    // U = Q D Z in global memory, reflectors j = n-2 .. 0 (one column per thread)
+    z* U = P.U;
+    for (int e = tid; e < n * k; e += VNT) {
+      const int rr = e / k, cc = e - rr * k;
+      U[e] = zsc(P.ph[rr], Z[(size_t)rr * lz + cc]);
+    }
+    __syncthreads();
+    for (int j = n - 2; j >= 0; --j) {
+      const double t = P.tau[j];
+      if (t == 0.0) continue;
+      const z* u = P.A + j;
+      for (int cc = tid; cc < k; cc += VNT) {
+        z s = mk(0, 0);
+        for (int rr = j + 1; rr < n; ++rr) s = zadd(s, zcjmul(u[(size_t)rr * n], U[(size_t)rr * k + cc]));
+        s = zsc(s, t);
+        for (int rr = j + 1; rr < n; ++rr) U[(size_t)rr * k + cc] = zsub(U[(size_t)rr * k + cc], zmul(u[(size_t)rr * n], s));
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // ---- fast path: U in registers.  Lane l of wave w: row chunk rc = l >> 2
+  // (rows i = 16 t + rc), column cc = l & 3 of the wave's column groups
+  // g = w, w + 8 (columns 4 g + cc); a reflector's dot products reduce over
+  // the 16 row chunks inside the wave, so reflectors need no barrier.
+  constexpr int TR = (RNMAX + 15) / 16;  // rows per lane (13)
+  constexpr int NG = 2;                  // column groups per wave (k <= 64)
+  const int rc = lane >> 2, cc = lane & 3;
+  z Ur[NG][TR];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int col = 4 * (wv + 8 * g) + cc;
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+      const int i = 16 * t + rc;
+      Ur[g][t] = (i < n && col < k) ? zsc(P.ph[i], Zl[(size_t)i * ldz + col]) : mk(0, 0);
+    }
+  }
+  const bool g0 = 4 * wv < k, g1 = 4 * (wv + 8) < k;  // wave-uniform
+  __syncthreads();  // Z no longer needed: the region now holds reflector blocks
+  z* Rb = (z*)un;   // [kRefBlk][RNMAX]: reflector jj of the block, rows 0..n-1 (zero at rows <= j)
+  __shared__ double stau[kRefBlk];
+  for (int jhi = n - 2; jhi >= 0; jhi -= kRefBlk) {
+    const int jlo = jhi - kRefBlk + 1 > 0 ? jhi - kRefBlk + 1 : 0;
+    const int nb = jhi - jlo + 1;
+    __syncthreads();  // previous block consumed
+    for (int e = tid; e < nb * n; e += VNT) {
+      const int rr = e / nb, jj = e - rr * nb, j = jlo + jj;
+      Rb[jj * RNMAX + rr] = rr > j ? P.A[(size_t)rr * n + j] : mk(0, 0);
+    }
+    for (int jj = tid; jj < nb; jj += VNT) stau[jj] = P.tau[jlo + jj];
+    __syncthreads();
+    if (!g0) continue;
+    for (int j = jhi; j >= jlo; --j) {
+      const double t = stau[j - jlo];
+      if (t == 0.0) continue;  // uniform
+      const z* u = Rb + (j - jlo) * RNMAX;
+      const int t0 = (j + 1) >> 4;  // first row slot holding rows > j (uniform)
+      z uu[TR];
+#pragma unroll
+      for (int tt = 0; tt < TR; ++tt) uu[tt] = (tt >= t0 && 16 * tt + rc < n) ? u[16 * tt + rc] : mk(0, 0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (g == 1 && !g1) continue;
+        z sacc = mk(0, 0);
+#pragma unroll
+        for (int tt = 0; tt < TR; ++tt) {
+          if (tt < t0) continue;
+          sacc.x = fma(uu[tt].x, Ur[g][tt].x, fma(uu[tt].y, Ur[g][tt].y, sacc.x));  // conj(u) U
+          sacc.y = fma(uu[tt].x, Ur[g][tt].y, fma(-uu[tt].y, Ur[g][tt].x, sacc.y));
+        }
+#pragma unroll
+        for (int o = 4; o < 64; o <<= 1) {
+          sacc.x += __shfl_xor(sacc.x, o, 64);
+          sacc.y += __shfl_xor(sacc.y, o, 64);
+        }
+        sacc = zsc(sacc, t);
+#pragma unroll
+        for (int tt = 0; tt < TR; ++tt) {
+          if (tt < t0) continue;
+          Ur[g][tt].x = fma(-uu[tt].x, sacc.x, fma(uu[tt].y, sacc.y, Ur[g][tt].x));
+          Ur[g][tt].y = fma(-uu[tt].x, sacc.y, fma(-uu[tt].y, sacc.x, Ur[g][tt].y));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int col = 4 * (wv + 8 * g) + cc;
+    if (col >= k) continue;
+#pragma unroll
+    for (int t = 0; t < TR; ++t) {
+      const int i = 16 * t + rc;
+      if (i < n) P.U[(size_t)i * k + col] = Ur[g][t];
+    }
+  }
+}
+
+}  // namespace hbm
