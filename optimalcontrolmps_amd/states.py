@@ -1,0 +1,42 @@
+"""Input states of the config-4 chains (host side, interchange format of
+include/ocmps.h).
+
+product_state: the reference's initial particle distribution
+    (include/InitializeState.hpp:26-40: "Occ1" on the Npart right-most sites,
+    "Emp" elsewhere) as an MPS with all bond dimensions 1.  For Npart = L it is
+    the Mott state |1...1>, config 4's psi_target.
+warm_state: config 4's psi_init — the product state evolved in real time at a
+    constant U until the bonds saturate at Maxm (the reference
+    prepares its states with ITensor DMRG, InitializeState.hpp:42-60, which is
+    out of scope here).  Runs on the given engine (the GPU stepper), not timed.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .native import MPS
+
+
+def product_state(L: int, p: int, npart: int) -> MPS:
+    """|0..0 1..1> with npart bosons on the right-most sites (InitializeState.hpp:26-40)."""
+    if npart > L:
+        raise ValueError("Npart > N not supported (include/InitializeState.hpp:29)")
+    Q1 = npart + 1
+    occ = [0] * (L - npart) + [1] * npart     # site k (1-based) holds occ[k-1]
+    dims = np.zeros((L + 1) * Q1, np.int32)
+    q = 0
+    dims[0 * Q1 + 0] = 1
+    for b in range(1, L + 1):
+        q += occ[b - 1]
+        dims[b * Q1 + q] = 1
+    return MPS(L, p, npart, dims, np.ones(L, np.complex128))
+
+
+def warm_state(engine, psi: MPS, U: float, nsteps: int, chunk: int = 50) -> MPS:
+    """nsteps forward steps at constant control U (BH_tDMRG::step, src/BH_tDMRG.cpp:111-125)."""
+    done = 0
+    while done < nsteps:
+        k = min(chunk, nsteps - done)
+        psi = engine.steps(psi, np.full(k + 1, float(U)), True)
+        done += k
+    return psi

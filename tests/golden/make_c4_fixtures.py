@@ -1,0 +1,81 @@
+"""Config-4 fixtures (TEST INFRASTRUCTURE): BASELINE configs[3]'s chain
+(L=20, Npart=20, d=6 -> p=7, tstep=0.005, cutoff 1e-8) on the CPU oracle.
+
+c4.npz:
+  s32/*   Maxm = 32 (binding): psi_init = the Mott state |1..1> evolved 200
+          steps at U = 2.5 by the oracle, psi_target = psi_init evolved 40
+          more steps at U = 6 (config 4's |1..1> target has ~1e-10 overlap
+          with psi_init, which would make every tolerance vacuous), N_t = 9
+          GRAPE controls U(2,10) (seed 4040): divT, F, gradient, full fidelity
+          Hessian (rows 1..7), fidelities.
+  w256/*  Maxm = 256: psi_init = tests/golden/c4_warm256.npz (the Mott state
+          evolved 400 steps at U = 2.5 on the GPU engine, bonds saturated at
+          256); one oracle step u 2.5 -> 3.0 forward: bond dims, <psi_0|psi_1>,
+          <psi_1|dH|psi_1>.
+Run: python tests/golden/make_c4_fixtures.py [s32] [w256]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+import oracle_ffi as O  # noqa: E402
+from optimalcontrolmps_amd.states import product_state  # noqa: E402
+
+L, p, N, J, DT, CUT = 20, 7, 20, 1.0, 0.005, 1e-8
+OUT = os.path.join(HERE, "c4.npz")
+
+
+def load_out():
+    return dict(np.load(OUT, allow_pickle=False)) if os.path.exists(OUT) else {}
+
+
+def make_s32(out):
+    maxm, Nt = 32, 9
+    st = O.Stepper(L, p, N, J, DT, CUT, maxm)
+    mott = product_state(L, p, N)
+    t0 = time.time()
+    psi = st.steps(O.MPS(L, p, N, mott.dims, mott.data), np.full(201, 2.5), True)
+    print(f"s32 warm-up: bonds {list(psi.bond_dims())} ({time.time() - t0:.1f}s)", flush=True)
+    tgt = st.steps(psi, np.full(41, 6.0), True)
+    u = np.random.default_rng(4040).uniform(2.0, 10.0, Nt)
+    oc = O.OC(st, tgt, psi, Nt, 0.0)
+    t0 = time.time()
+    H = oc.hessian(u, 8)
+    g = oc.gradient(u)
+    divT, F = oc.divT_F()
+    fid = oc.fidelities(u)
+    print(f"s32 oracle hessian+gradient {time.time() - t0:.1f}s  max|H| {np.abs(H).max():.3e} "
+          f"max|g| {np.abs(g).max():.3e}", flush=True)
+    out.update({"s32/init_dims": psi.dims, "s32/init_data": psi.data, "s32/tgt_dims": tgt.dims, "s32/tgt_data": tgt.data,
+                "s32/u": u, "s32/H": H, "s32/grad": g, "s32/divT": divT, "s32/F": np.array([F]),
+                "s32/fid": fid, "s32/maxm": np.array(maxm)})
+
+
+def make_w256(out):
+    z = np.load(os.path.join(HERE, "c4_warm256.npz"), allow_pickle=False)
+    st = O.Stepper(L, p, N, J, DT, CUT, 256)
+    psi0 = O.MPS(L, p, N, z["dims"], z["data"])
+    t0 = time.time()
+    psi1 = st.steps(psi0, np.array([2.5, 3.0]), True)
+    ov = st.overlap(psi0, psi1)
+    dh = st.overlap_dH(psi1, psi1)
+    print(f"w256 oracle step {time.time() - t0:.1f}s bonds {list(psi1.bond_dims())} <0|1> {ov} <1|dH|1> {dh}",
+          flush=True)
+    out.update({"w256/bonds1": np.asarray(psi1.bond_dims()), "w256/ov01": np.array([ov]),
+                "w256/dH11": np.array([dh])})
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["s32", "w256"]
+    out = load_out()
+    if "s32" in which:
+        make_s32(out)
+    if "w256" in which:
+        make_w256(out)
+    np.savez_compressed(OUT, **out)

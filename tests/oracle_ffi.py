@@ -97,7 +97,7 @@ class Stepper:
         self.L, self.p, self.Q = L, p, Q
         self.J, self.dt, self.cutoff, self.maxm = J, dt, cutoff, maxm
         self.h = lib().orc_new(L, p, Q, J, dt, cutoff, maxm)
-        self.cap = 1 << 18
+        self.cap = 1 << 21  # complex elements (a saturated chi = 256 config-4 chain has ~5e5)
 
     def __del__(self):
         try:

@@ -1,0 +1,120 @@
+"""BASELINE configs[3]'s chain on the HBM-resident engine: L=20, Npart=20,
+d=6 (p=7), tstep=0.005, cutoff 1e-8.
+
+* s32: Maxm 32 (binding), N_t = 9: divT, F, gradient and the full fidelity
+  Hessian against the oracle's golden vectors (tests/golden/c4.npz, made by
+  tests/golden/make_c4_fixtures.py) at the north_star tolerances (gradient
+  1e-6 absolute, Hessian 1e-6 max|H|).
+* w256: Maxm 256 from the saturated warm state (tests/golden/c4_warm256.npz):
+  one step against the oracle's (bond dimensions, <psi_0|psi_1>,
+  <psi_1|dH|psi_1>), batched steps bitwise equal to single-chain steps, and
+  the analytic gradient against central differences of the cost (the
+  reference's GradientTests criterion, 0.1 %, tests/GradientTests.cpp:140-143).
+"""
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+L, p, N, J, DT, CUT = 20, 7, 20, 1.0, 0.005, 1e-8
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c4():
+    return dict(np.load(os.path.join(HERE, "golden", "c4.npz"), allow_pickle=False))
+
+
+@pytest.fixture(scope="module")
+def warm256():
+    from optimalcontrolmps_amd.native import MPS
+    z = np.load(os.path.join(HERE, "golden", "c4_warm256.npz"), allow_pickle=False)
+    return MPS(L, p, N, z["dims"], z["data"])
+
+
+def _mps(dims, data):
+    from optimalcontrolmps_amd.native import MPS
+    return MPS(L, p, N, dims, data)
+
+
+def test_c4_s32_vs_oracle(c4):
+    from optimalcontrolmps_amd.native import Engine
+    u = c4["s32/u"]
+    Nt = len(u)
+    eng = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+    eng.set_states(_mps(c4["s32/tgt_dims"], c4["s32/tgt_data"]), _mps(c4["s32/init_dims"], c4["s32/init_data"]))
+    eng.propagate(u, 3)
+    divT = eng.div_t()
+    F = eng.overlap_factor()
+    fid = eng.fidelities()
+    eng.xi_dH()
+    H = eng.hessian_rows(u, list(range(1, Nt - 1)), F, divT)
+    g = DT * (divT * F * 1j).real
+    Fo, go, Ho = complex(c4["s32/F"][0]), c4["s32/grad"], c4["s32/H"]
+    assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12
+    assert np.abs(divT - c4["s32/divT"]).max() <= 1e-8 * np.abs(c4["s32/divT"]).max()
+    assert np.abs(fid - c4["s32/fid"]).max() <= 1e-10
+    # north_star tolerances, and far tighter in practice
+    assert np.abs(g - go).max() <= 1e-6
+    assert np.abs(g - go).max() <= 1e-7 * np.abs(go).max()
+    assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+    eng.close()
+
+
+def test_c4_w256_step_vs_oracle(c4, warm256):
+    from optimalcontrolmps_amd.native import Engine
+    if "w256/bonds1" not in c4:
+        pytest.skip("w256 oracle fixture not generated")
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    psi1 = eng.steps(warm256, np.array([2.5, 3.0]), True)
+    assert list(psi1.bond_dims()) == list(c4["w256/bonds1"])
+    ov = eng.overlap(warm256, psi1)
+    dh = eng.overlap(psi1, psi1, True)
+    assert abs(ov - complex(c4["w256/ov01"][0])) <= 1e-10
+    assert abs(dh - complex(c4["w256/dH11"][0])) <= 1e-9 * abs(complex(c4["w256/dH11"][0]))
+    assert abs(eng.overlap(psi1, psi1) - 1.0) <= 1e-12
+    eng.close()
+
+
+def test_c4_w256_batched_equals_single(warm256):
+    """ocg_step_batch over differently-driven chains == one ocg_step each (bitwise):
+    a chain's arithmetic does not depend on what else is in the batch."""
+    from optimalcontrolmps_amd.native import Engine
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    uf, ut = np.array([2.5, 4.0, 9.0]), np.array([3.0, 2.0, 7.5])
+    states = [warm256, warm256, eng.step(warm256, 2.5, 5.0)]
+    batched = eng.step_batch(states, uf, ut, True)
+    for i, s in enumerate(states):
+        single = eng.step(s, uf[i], ut[i], True)
+        assert np.array_equal(single.dims, batched[i].dims)
+        assert np.array_equal(single.data, batched[i].data)
+    eng.close()
+
+
+def test_c4_w256_gradient_fd(warm256):
+    """getAnalyticGradient (GRAPE, psi and xi on the device, divT) against central
+    differences of calcCost over a short horizon at chi = 256."""
+    from optimalcontrolmps_amd.native import Engine
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    Nt = 4
+    tgt = eng.steps(warm256, np.full(3, 6.0), True)  # overlapping target (see tests/golden/make_c4_fixtures.py)
+    u = np.random.default_rng(5).uniform(2.0, 10.0, Nt)
+    eng.set_states(tgt, warm256)
+
+    def cost(v):
+        eng.propagate(v, 1)
+        F = eng.overlap_factor()
+        return 0.5 * (1.0 - abs(F) ** 2)
+
+    eng.propagate(u, 3)
+    g = DT * (eng.div_t() * eng.overlap_factor() * 1j).real
+    eps = 1e-4
+    for i in range(1, Nt - 1):
+        up, um = u.copy(), u.copy()
+        up[i] += eps
+        um[i] -= eps
+        num = (cost(up) - cost(um)) / (2 * eps)
+        assert abs(g[i] - num) <= 1e-3 * abs(num) + 1e-12, (i, g[i], num)
+    eng.close()
