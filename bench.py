@@ -20,6 +20,20 @@ assembly.  Multi-GPU (one process per GPU):
                 the critical path (~200 steps) does not shrink with N.
 
 value = Hessian rows completed per second (whole job).
+
+Other workloads (--workload; one JSON line each, not the driver's default):
+  gradient   config 2: getAnalyticGradient with BFGS=true (psi and xi chains
+             concurrently, divT, F; src/OptimalControl.cpp:204-249) at config 1,
+             value = gradients/s.
+  c4grad     config 4 chain (L=20 Npart=20 d=6 chi=256 tstep=0.005): one
+             getAnalyticGradient over the full horizon T=4 (N_t=801) from the
+             saturated warm state, value = gradients/s (+ sweep-steps/s).
+  c4rows     config 4 chain: getHessian fidelity part over a T slice
+             (--c4-nt time points, default 33: all N_t-2 rows), value = rows/s.
+The roofline block names the limiter honestly: config 1 is latency-bound (one
+chain's 200 dependent steps on one CU, state in LDS), so `frac` is reported
+against HBM for the contract but the measured HBM bytes (rocprofv3 PMC,
+profiles/) sit next to the model bytes.
 """
 import argparse
 import json
@@ -46,7 +60,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c4rows"], default="hessian")
+    ap.add_argument("--c4-nt", type=int, default=33)
+    ap.add_argument("--profile-tag", default="r02")
     args = ap.parse_args()
+    if args.workload in ("c4grad", "c4rows"):
+        return bench_c4(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -76,6 +95,9 @@ def main():
     eng = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
     eng.set_states(tgt, ini)
     Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=dev)
+
+    if args.workload == "gradient":
+        return bench_gradient(args, eng, u, Nt, dt, world, rank, dist, dev)
 
     def one_step():
         # fused getHessian: psi/xi chains, xiHlist and this rank's rows in one
@@ -111,7 +133,9 @@ def main():
     value = rows_total / elapsed
     st_rows = eng.stats(5)       # k_pipeline: trajectories + row re-propagation (dominant)
     st_ovl = eng.stats(6)        # k_row_overlaps
-    st_traj = eng.stats(0)
+    t_tr = time.perf_counter()
+    eng.propagate(u, 3)          # one bare psi || xi trajectory (outside the timed region): single-chain step rate
+    t_tr = time.perf_counter() - t_tr
     row_steps = (Nt - 2) * (Nt - 3) // 2
     sweep_steps = args.steps * (2 * (Nt - 1) * world + row_steps * (1 if strong else world))
     result = None
@@ -144,18 +168,11 @@ def main():
                 "row_overlaps": {"avg_ms": st_ovl["ms"] / max(1, st_ovl["launches"]), "launches": st_ovl["launches"]},
                 "divT_F_overlaps_ms": eng.stats(1)["ms"] / max(1, args.steps),
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_pipeline",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": measured_traffic("k_pipeline"),
-                "alg_bytes_per_launch": bytes_per_launch,
-                "fp64_achieved_tflops": flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0,
-                "fp64_peak_tflops": FP64_PEAK_TFS,
-            },
+            "single_chain_steps_per_sec": (Nt - 1) / t_tr,
+            "roofline": roofline_block("k_pipeline", launch_ms, bytes_per_launch, flops_per_launch,
+                                       args.profile_tag,
+                                       limiter="issue latency: one chain's N_t-1 dependent steps on one CU "
+                                               "(state in LDS); HBM and FP64 are both <1% busy"),
         }
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(ini, tgt, u, args.cpu_threads)
@@ -163,6 +180,171 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def st_traj_ms_per_step(eng, Nt):
+    """ms per step of one chain: the bare two-chain trajectory (ocg_propagate(u, 3))
+    timed once outside the measured region (the pipeline's critical path)."""
+    st = eng.stats(0)
+    if st["launches"] == 0:
+        return 0.0
+    return st["ms"] / st["launches"] / (Nt - 1)
+
+
+def roofline_block(kernel, launch_ms, bytes_per_launch, flops_per_launch, tag, limiter, bound="hbm"):
+    """Roofline of the dominant kernel.  achieved = algorithmic bytes (SURVEY.md
+    §8d model) / HIP-event launch time; traffic = HBM bytes
+    per dispatch measured by rocprofv3 PMC (profiles/<tag>_summary.json, FETCH_SIZE
+    doubled per the gfx950 calibration) and its own fraction of peak."""
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    traffic = measured_traffic(kernel, tag)
+    meas = traffic / (launch_ms * 1e-3) / 1e9 if (traffic and launch_ms > 0) else None
+    return {
+        "bound": bound,
+        "limiter": limiter,
+        "kernel": kernel,
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "measured_hbm_gbs": meas,
+        "measured_frac": (meas / HBM_PEAK_GBS) if meas is not None else None,
+        "alg_bytes_per_launch": bytes_per_launch,
+        "avg_launch_ms": launch_ms,
+        "fp64_achieved_tflops": flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0,
+        "fp64_peak_tflops": FP64_PEAK_TFS,
+    }
+
+
+def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, dev):
+    """config 2: getAnalyticGradient(u) with BFGS=true at config 1 — psi_t and xi_t
+    propagated concurrently in one launch (calcFidelityGrad's BFGS branch,
+    src/OptimalControl.cpp:217-229, propagates xi independently of psi), then the
+    batched divT overlaps and F (ocg_propagate(u, 3) + ocg_div_t + ocg_overlap_factor)."""
+    import torch
+
+    def one():
+        eng.propagate(u, 3)
+        divT = eng.div_t()
+        F = eng.overlap_factor()
+        return dt * (divT * F * 1j).real
+
+    for _ in range(args.warmup):
+        one()
+    eng.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st_traj, st_ov = eng.stats(0), eng.stats(1)
+    if rank == 0:
+        launch_ms = st_traj["ms"] / max(1, st_traj["launches"])
+        res = {
+            "metric": "getAnalyticGradient/sec (BFGS=true: psi || xi + divT), N=5 d=4 chi=80 T=2.0",
+            "value": args.steps * world / elapsed, "unit": "gradients/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c128/f64",
+            "data": "synthetic GRAPE controls U(2,10) seed 20261015; ED ground states U=2.5 -> 50",
+            "config": {"workload": "config 2: getAnalyticGradient(u, new_control=true), BFGS=true, N_t=201"},
+            "sweep_steps_per_sec": args.steps * world * 2 * (Nt - 1) / elapsed,
+            "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(launch_ms, 1e-9),
+            "kernels": {"trajectory_ms": launch_ms, "divT_F_ms": st_ov["ms"] / max(1, args.steps)},
+            "roofline": roofline_block("k_trajectory", launch_ms, st_traj["alg_bytes"] / max(1, st_traj["launches"]),
+                                       st_traj["alg_flops"] / max(1, st_traj["launches"]), args.profile_tag,
+                                       limiter="issue latency: 200 dependent steps per chain, one CU per chain"),
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+C4 = dict(L=20, p=7, npart=20, J=1.0, tstep=0.005, T=4.0, maxm=256, cutoff=1e-8, seed=20261016)
+
+
+def bench_c4(args):
+    """Config 4's chain (BASELINE configs[3]: L=20 Npart=20 d=6 chi=256 tstep=0.005
+    T=4) on the HBM-resident engine, one GPU.  psi_init = the saturated warm state
+    (tests/golden/c4_warm256.npz: |1..1> evolved 400 steps at U=2.5, bonds 256),
+    psi_target = psi_init evolved 2 more steps at U=6 (config 4's |1..1> target has
+    ~1e-10 overlap, which leaves every derivative at rounding level; cost is
+    independent of the target).  GRAPE controls U(2,10); the GROUP M=40 projection
+    is a host GEMM (ControlBasis) and not part of the timed device work."""
+    import torch
+    from optimalcontrolmps_amd.native import MPS, Engine
+    c = C4
+    L, p, Q, dt = c["L"], c["p"], c["npart"], c["tstep"]
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c4_warm256.npz"), allow_pickle=False)
+    ini = MPS(L, p, Q, z["dims"], z["data"])
+    eng = Engine(L, p, Q, c["J"], dt, c["cutoff"], c["maxm"], device=0, engine="hbm")
+    tgt = eng.steps(ini, np.full(3, 6.0), True)
+    eng.set_states(tgt, ini)
+    grad = args.workload == "c4grad"
+    Nt = int(round(c["T"] / dt)) + 1 if grad else args.c4_nt
+    u = np.random.default_rng(c["seed"]).uniform(2.0, 10.0, Nt)
+    rows = list(range(1, Nt - 1))
+
+    def one():
+        if grad:
+            eng.propagate(u, 3)
+            divT = eng.div_t()
+            F = eng.overlap_factor()
+            return dt * (divT * F * 1j).real
+        eng.propagate(u, 3)
+        divT = eng.div_t()
+        F = eng.overlap_factor()
+        eng.xi_dH()
+        return eng.hessian_rows(u, rows, F, divT)
+
+    for _ in range(args.warmup):
+        one()
+    eng.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    gm = eng.stats(7)   # k_gemm: the MFMA-FP64 contraction kernel
+    st_traj = eng.stats(0)
+    steps_traj = 2 * (Nt - 1)
+    row_steps = (Nt - 2) * (Nt - 3) // 2
+    sweep = args.steps * (steps_traj + (0 if grad else row_steps))
+    gemm_ms = gm["ms"] / max(1, gm["launches"])
+    res = {
+        "metric": ("getAnalyticGradient/sec (psi || xi + divT)" if grad else "Hessian-rows/sec (getHessian fidelity part)")
+                  + ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005",
+        "value": (args.steps if grad else args.steps * (Nt - 2)) / elapsed,
+        "unit": "gradients/s" if grad else "rows/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c128/f64",
+        "data": "synthetic GRAPE controls U(2,10) seed 20261016; psi_init = saturated chi=256 warm state",
+        "config": {"workload": (f"config 4 chain, getAnalyticGradient over N_t={Nt} (T=4)" if grad else
+                                f"config 4 chain, getHessian over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)"),
+                   "engine": "HBM-resident (hbm.hip)"},
+        "sweep_steps_per_sec": sweep / elapsed,
+        "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(st_traj["ms"] / max(1, st_traj["launches"]), 1e-9),
+        "mfma_gemm": {"kernel": "k_gemm (v_mfma_f64_16x16x4f64)", "launches_per_step": gm["launches"] / args.steps,
+                      "avg_launch_ms": gemm_ms, "share_of_time": gm["ms"] / (1e3 * elapsed),
+                      "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,
+                      "achieved_gbs": gm["alg_bytes"] / max(gm["ms"], 1e-9) / 1e6},
+        "roofline": roofline_block("k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
+                                   gm["alg_flops"] / max(1, gm["launches"]), args.profile_tag,
+                                   limiter="the per-sector Hermitian eigensolver (k_heev_*: one CU per block, "
+                                           "latency-bound), not the MFMA contraction"),
+    }
+    print(json.dumps(res), flush=True)
 
 
 def measured_traffic(kernel, tag="r01"):

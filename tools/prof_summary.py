@@ -40,10 +40,10 @@ def pmc(db, counter):
     return out
 
 
-def main(tag):
+def main(tag, outdir=None):
     g = os.path.join(ROOT, "gpurun_out")
     ks = kernel_stats(os.path.join(g, f"prof_{tag}", "run_results.db"))
-    prof = os.path.join(ROOT, "profiles")
+    prof = outdir or os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=["kernel", "calls", "total_ms", "avg_ms", "pct"])
@@ -64,9 +64,17 @@ def main(tag):
             corrected = 2.0 * f_kb * 1024 + w_kb * 1024
             per[k] = dict(dispatches=fk[1], fetch_kb=f_kb, write_kb=w_kb, hbm_bytes=corrected)
             w.writerow([k, fk[1], f"{f_kb:.3f}", f"{w_kb:.3f}", f"{corrected:.0f}"])
-    summary = dict(tag=tag, kernels=ks, pmc_per_dispatch=per,
-                   note="rocprofv3 --kernel-trace --stats and separate --pmc FETCH_SIZE / WRITE_SIZE passes of "
-                        "`python3 bench.py` (config 1); FETCH_SIZE doubled per the gfx950 calibration")
+    extra = {}
+    mdb = os.path.join(g, f"pmc_mfma_{tag}", "run_results.db")
+    if os.path.exists(mdb):
+        for cn in ("SQ_INSTS_VALU_MFMA_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
+                   "SQ_INSTS_VALU_FMA_F64", "GRBM_GUI_ACTIVE"):
+            for k, (v, n) in pmc(mdb, cn).items():
+                extra.setdefault(k, {})[cn + "_per_dispatch"] = v / n
+    summary = dict(tag=tag, kernels=ks, pmc_per_dispatch=per, pmc_issue=extra,
+                   note="rocprofv3 --kernel-trace --stats and separate --pmc passes (FETCH_SIZE, WRITE_SIZE, "
+                        "MFMA/issue counters) of the same `python3 bench.py` command; FETCH_SIZE doubled per the "
+                        "gfx950 calibration")
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps({k: v for k, v in per.items() if k.startswith("k_")}, indent=1))
@@ -75,4 +83,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else None)
