@@ -339,8 +339,8 @@ def bench_c4(args):
                       "avg_launch_ms": gemm_ms, "share_of_time": gm["ms"] / (1e3 * elapsed),
                       "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,
                       "achieved_gbs": gm["alg_bytes"] / max(gm["ms"], 1e-9) / 1e6},
-        "roofline": roofline_block("k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
-                                   gm["alg_flops"] / max(1, gm["launches"]), args.profile_tag,
+        "roofline": roofline_block("hbm::k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
+                                   gm["alg_flops"] / max(1, gm["launches"]), args.profile_tag + "c4",
                                    limiter="the per-sector Hermitian eigensolver (k_heev_*: one CU per block, "
                                            "latency-bound), not the MFMA contraction"),
     }

@@ -471,7 +471,77 @@ __global__ __launch_bounds__(RNT, 1) void k_heev_vals_any(const EProb* __restric
 // registers (lane = column, rows i = 8a + wave) and the reflectors applied
 // j = n-2 .. 0 from LDS blocks.  Other sizes: the same algorithm with Z and
 // U in global memory.
-constexpr int kVecLds = 110592;  // bytes of the Z / reflector-block region
+constexpr int kVecLds = 143360;  // bytes of the Z + pivot / Gram / reflector-block region
+// Inverse iteration for lane-parallel eigenvectors with the pivots in LDS
+// (column jd of Dv, ld ldd): pivots by a refined reciprocal, the forward and
+// backward sweeps unrolled by 4 with their loads issued ahead of the
+// dependent FMA chain (one wave carries the whole batch: no other wave hides
+// LDS latency).
+__device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const double* __restrict__ Le, int n,
+                                           double lam, double tiny, double* __restrict__ Z, int ldz, int jz,
+                                           double* __restrict__ Dv, int ldd, int jd, int jj) {
+  double q = Ld[0] - lam;
+  if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
+  Dv[jd] = q;
+  for (int i = 1; i < n; ++i) {
+    double r = __builtin_amdgcn_rcp(q);
+    r = fma(r, fma(-q, r, 1.0), r);
+    q = fma(-Le[i - 1] * Le[i - 1], r, Ld[i] - lam);
+    if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
+    Dv[(size_t)i * ldd + jd] = q;
+  }
+  for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] = hrand(i, jj);
+  for (int it = 0; it < 3; ++it) {
+    // forward: y_i = b_i - (e_{i-1} / q_{i-1}) y_{i-1}
+    double y = Z[jz];
+    int i = 1;
+    for (; i + 3 < n; i += 4) {
+      double b[4], l[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        b[t] = Z[(size_t)(i + t) * ldz + jz];
+        l[t] = Le[i + t - 1] / Dv[(size_t)(i + t - 1) * ldd + jd];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        y = fma(-l[t], y, b[t]);
+        Z[(size_t)(i + t) * ldz + jz] = y;
+      }
+    }
+    for (; i < n; ++i) {
+      y = fma(-Le[i - 1] / Dv[(size_t)(i - 1) * ldd + jd], y, Z[(size_t)i * ldz + jz]);
+      Z[(size_t)i * ldz + jz] = y;
+    }
+    // backward: x_i = (y_i - e_i x_{i+1}) / q_i
+    double xn = Z[(size_t)(n - 1) * ldz + jz] / Dv[(size_t)(n - 1) * ldd + jd];
+    Z[(size_t)(n - 1) * ldz + jz] = xn;
+    double ss = xn * xn;
+    i = n - 2;
+    for (; i - 3 >= 0; i -= 4) {
+      double b[4], e[4], rq[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        b[t] = Z[(size_t)(i - t) * ldz + jz];
+        e[t] = Le[i - t];
+        rq[t] = 1.0 / Dv[(size_t)(i - t) * ldd + jd];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        xn = fma(-e[t], xn, b[t]) * rq[t];
+        Z[(size_t)(i - t) * ldz + jz] = xn;
+        ss = fma(xn, xn, ss);
+      }
+    }
+    for (; i >= 0; --i) {
+      xn = (Z[(size_t)i * ldz + jz] - Le[i] * xn) / Dv[(size_t)i * ldd + jd];
+      Z[(size_t)i * ldz + jz] = xn;
+      ss = fma(xn, xn, ss);
+    }
+    const double inv = ss > 0 ? 1.0 / sqrt(ss) : 0.0;
+    for (int t = 0; t < n; ++t) Z[(size_t)t * ldz + jz] *= inv;
+  }
+}
+
 constexpr int kVecRows = (RNMAX + VNT / 64 - 1) / (VNT / 64);  // rows per thread (fast path)
 constexpr int kRefBlk = 24;                   // reflectors per LDS block
 
@@ -522,11 +592,11 @@ __device__ __forceinline__ void invit(const double* Ld, const double* Le, int n,
     for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] *= inv;
   }
 }
-constexpr int kInvBatch = 16;  // eigenvectors per inverse-iteration batch (fast path: LDS pivots)
+
 
 __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__ probs, int nprob) {
   __shared__ __align__(16) char un[kVecLds];
-  __shared__ double Lpiv[RNMAX * kInvBatch];
+  __shared__ int chol_fail;
   __shared__ double Ld[RNMAX], Le[RNMAX], Lc[64];
   __shared__ z part[VNT / 64][64];
   __shared__ double red[VNT / 64];
@@ -540,7 +610,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
     return;
   }
   const int ldz = k + 1;  // odd stride: row reads of Z by consecutive threads hit distinct banks
-  const bool fast = n <= RNMAX && k <= 64 && size_t(n) * ldz * 8 <= size_t(kVecLds);
+  const bool fast = n <= RNMAX && k <= 64 && (size_t(n) * ldz + size_t(n) + 64 * 65) * 8 <= size_t(kVecLds);
   double* Zl = (double*)un;
   // generic path: the tridiagonal in global memory scratch (P.d / P.e), Z and U global
   const double* Gd = P.d;
@@ -560,54 +630,127 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
   for (int q = 1; q < VNT / 64; ++q) tn = fmax(tn, red[q]);
   __syncthreads();
   const double tiny = 2.220446049250313e-16 * fmax(tn, 1e-300);
+#ifdef HBM_STAMP
+  unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
+#endif
   double* Z = fast ? Zl : P.Z;
   const int lz = fast ? ldz : n;
   if (fast) {
-    for (int jb = 0; jb < k; jb += kInvBatch) {
+    // pivots in the region's tail after Z: as many eigenvectors per batch as fit (all of them when k <= 64
+    // and n (k + 1 + k) doubles fit)
+    double* piv = Zl + (size_t)n * ldz;
+    const int room = int((size_t(kVecLds) / 8 - (size_t)n * ldz) / size_t(n));
+    const int batch = room < k ? (room < 1 ? 1 : room) : k;
+    for (int jb = 0; jb < k; jb += batch) {
       const int jj = jb + tid;
-      if (tid < kInvBatch && jj < k) invit(Ld, Le, n, P.w[jj], tiny, Zl, ldz, jj, Lpiv, kInvBatch, tid, jj);
+      if (tid < batch && jj < k) invit_fast(Ld, Le, n, P.w[jj], tiny, Zl, ldz, jj, piv, batch, tid, jj);
     }
   } else {
     for (int jj = tid; jj < k; jj += VNT) invit(Gd, Ge, n, P.w[jj], tiny, Z, lz, jj, P.Dv, n, jj, jj);
   }
   __syncthreads();
-  // classical Gram-Schmidt, twice, descending; dots split over 8 row chunks
-  double* Lcf = fast ? Lc : P.tau + n;  // generic: coefficient scratch must hold k (see decompose_eig sizing)
-  (void)Lcf;
-  for (int j = 1; j < k; ++j) {
-    for (int pass = 0; pass < 2; ++pass) {
-      // part[ch][i] = sum_{r = ch mod 8} Z[r][i] Z[r][j]
-      for (int i0 = 0; i0 < j; i0 += 64) {
-        const int i = i0 + lane;
-        double pa = 0;
-        if (i < j)
-          for (int rr = wv; rr < n; rr += VNT / 64) pa += Z[(size_t)rr * lz + i] * Z[(size_t)rr * lz + j];
-        part[wv][lane].x = pa;
-        __syncthreads();
-        if (tid < 64 && i < j) {
-          double sc = 0;
+  STAMP(0);
+  // Orthonormalise the k inverse-iteration vectors.  Fast path: CholeskyQR2
+  // (G = Z^T Z over all threads, G = L L^T by one wave, Z <- Z L^-T row by
+  // row, twice); a collapsed Cholesky pivot (nearly dependent vectors) falls
+  // back to classical Gram-Schmidt, twice, which any path can take.
+  bool need_gs = !fast || k > 64;
+  if (!need_gs) {
+    double* G = Zl + (size_t)n * ldz;  // k x k (ld 65), lower triangle, after Z (pivots no longer needed)
+    for (int pass = 0; pass < 2 && !need_gs; ++pass) {
+      // G = Z^T Z: task (i, jb) sums columns 8 jb .. 8 jb + 7 (<= i) against column i
+      const int nb8 = (k + 7) >> 3;
+      for (int task = tid; task < k * nb8; task += VNT) {
+        const int i = task / nb8, jb = task - i * nb8;
+        if (8 * jb > i) continue;
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int rr = 0; rr < n; ++rr) {
+          const double* zr = Zl + (size_t)rr * ldz;
+          const double zi = zr[i];
 #pragma unroll
-          for (int q = 0; q < VNT / 64; ++q) sc += part[q][tid].x;
-          part[0][tid].y = sc;
+          for (int t = 0; t < 8; ++t) acc[t] = fma(zi, zr[8 * jb + t < k ? 8 * jb + t : 0], acc[t]);
         }
-        __syncthreads();
-        // Z[r][j] -= sum_{i in this chunk} c_i Z[r][i]
-        for (int rr = tid; rr < n; rr += VNT) {
-          double s = 0;
-          const int ie = j - i0 < 64 ? j - i0 : 64;
-          for (int q = 0; q < ie; ++q) s += part[0][q].y * Z[(size_t)rr * lz + i0 + q];
-          Z[(size_t)rr * lz + j] -= s;
-        }
-        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if (8 * jb + t <= i) G[i * 65 + 8 * jb + t] = acc[t];
       }
+      if (tid == 0) chol_fail = 0;
+      __syncthreads();
+      if (wv == 0) {
+        // right-looking Cholesky, lane i owns row i
+        for (int cc = 0; cc < k; ++cc) {
+          const double dgg = G[cc * 65 + cc];
+          if (!(dgg > 1e-10)) {  // columns are unit vectors: a pivot this small means a near dependency
+            if (lane == 0) chol_fail = 1;
+            break;
+          }
+          const double dd = sqrt(dgg);
+          if (lane == cc) G[cc * 65 + cc] = dd;
+          const double lic = (lane > cc && lane < k) ? G[lane * 65 + cc] / dd : 0.0;
+          if (lane > cc && lane < k) G[lane * 65 + cc] = lic;
+          __builtin_amdgcn_wave_barrier();
+          // trailing update, uniform trip count so the independent LDS loads pipeline
+#pragma unroll 8
+          for (int jj = cc + 1; jj < k; ++jj) {
+            const double ljc = G[jj * 65 + cc];
+            if (jj <= lane && lane < k) G[lane * 65 + jj] = fma(-lic, ljc, G[lane * 65 + jj]);
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      __syncthreads();
+      if (chol_fail) { need_gs = true; break; }
+      // Z[r][:] <- Z[r][:] L^-T: forward substitution along the row
+      for (int rr = tid; rr < n; rr += VNT) {
+        double* zr = Zl + (size_t)rr * ldz;
+        for (int jj = 0; jj < k; ++jj) {
+          double acc = zr[jj];
+          for (int i = 0; i < jj; ++i) acc = fma(-zr[i], G[jj * 65 + i], acc);
+          zr[jj] = acc / G[jj * 65 + jj];
+        }
+      }
+      __syncthreads();
     }
-    double ss = 0;
-    for (int rr = tid; rr < n; rr += VNT) { const double v = Z[(size_t)rr * lz + j]; ss += v * v; }
-    ss = block_sum_r(ss, red);
-    const double inv = ss > 0 ? 1.0 / sqrt(ss) : 0.0;
-    for (int rr = tid; rr < n; rr += VNT) Z[(size_t)rr * lz + j] *= inv;
-    __syncthreads();
   }
+  if (need_gs) {
+    // classical Gram-Schmidt, twice, descending; dots split over 8 row chunks
+    for (int j = 0; j < k; ++j) {
+      for (int pass = 0; pass < 2 && j > 0; ++pass) {
+        // part[ch][i] = sum_{r = ch mod 8} Z[r][i] Z[r][j]
+        for (int i0 = 0; i0 < j; i0 += 64) {
+          const int i = i0 + lane;
+          double pa = 0;
+          if (i < j)
+            for (int rr = wv; rr < n; rr += VNT / 64) pa += Z[(size_t)rr * lz + i] * Z[(size_t)rr * lz + j];
+          part[wv][lane].x = pa;
+          __syncthreads();
+          if (tid < 64 && i < j) {
+            double sc = 0;
+#pragma unroll
+            for (int q = 0; q < VNT / 64; ++q) sc += part[q][tid].x;
+            part[0][tid].y = sc;
+          }
+          __syncthreads();
+          // Z[r][j] -= sum_{i in this chunk} c_i Z[r][i]
+          for (int rr = tid; rr < n; rr += VNT) {
+            double s = 0;
+            const int ie = j - i0 < 64 ? j - i0 : 64;
+            for (int q = 0; q < ie; ++q) s += part[0][q].y * Z[(size_t)rr * lz + i0 + q];
+            Z[(size_t)rr * lz + j] -= s;
+          }
+          __syncthreads();
+        }
+      }
+      double ss = 0;
+      for (int rr = tid; rr < n; rr += VNT) { const double v = Z[(size_t)rr * lz + j]; ss += v * v; }
+      ss = block_sum_r(ss, red);
+      const double inv = ss > 0 ? 1.0 / sqrt(ss) : 0.0;
+      for (int rr = tid; rr < n; rr += VNT) Z[(size_t)rr * lz + j] *= inv;
+      __syncthreads();
+    }
+  }
+  STAMP(1);
   if (!fast) {
     // U = Q D Z in global memory, reflectors j = n-2 .. 0 (one column per thread)
     z* U = P.U;
@@ -649,6 +792,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
   }
   const bool g0 = 4 * wv < k, g1 = 4 * (wv + 8) < k;  // wave-uniform
   __syncthreads();  // Z no longer needed: the region now holds reflector blocks
+  STAMP(2);
   z* Rb = (z*)un;   // [kRefBlk][RNMAX]: reflector jj of the block, rows 0..n-1 (zero at rows <= j)
   __shared__ double stau[kRefBlk];
   for (int jhi = n - 2; jhi >= 0; jhi -= kRefBlk) {
@@ -661,6 +805,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
     }
     for (int jj = tid; jj < nb; jj += VNT) stau[jj] = P.tau[jlo + jj];
     __syncthreads();
+    STAMP(3);
     if (!g0) continue;
     for (int j = jhi; j >= jlo; --j) {
       const double t = stau[j - jlo];
@@ -694,7 +839,12 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
         }
       }
     }
+    STAMP(4);
   }
+#ifdef HBM_STAMP
+  if (tid == 0)
+    for (int q = 0; q < 8; ++q) P.Z[q] = double(stamp_acc[q]);
+#endif
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
     const int col = 4 * (wv + 8 * g) + cc;

@@ -112,6 +112,14 @@ int main(int argc, char** argv) {
     printf("stamps (wave 0, s_memtime ticks, last rep):");
     for (int q = 0; q < 8; ++q) printf(" %s %.0f (%.0f%%)", nm[q], st[q], 100 * st[q] / tot);
     printf(" | per column %.0f\n", tot / (n - 1));
+    // vecs kernel stamps (written after the vals ones were read: rerun vecs once)
+    hipLaunchKernelGGL(k_heev_vecs_reg, dim3(B), dim3(VNT), 0, 0, dP, B);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(st.data(), dZ, 64, hipMemcpyDeviceToHost));
+    const char* nv[5] = {"invit", "orth", "U init", "BT loads", "BT apply"};
+    printf("vecs stamps:");
+    for (int q = 0; q < 5; ++q) printf(" %s %.0f", nv[q], st[q]);
+    printf("\n");
   }
 #endif
   printf("n=%d B=%d k=%d: vals %.1f us  vecs %.1f us per launch | max|A u - w u|/w0 = %.2e  orth %.2e  "
