@@ -522,6 +522,32 @@ static void scen_nlp(Json& js) {
   js.num("u_initial_mid", uI[N / 2]);
 }
 
+// BASELINE configs[2] (config 3) at config 1's shape: L=5 Npart=5 d=4 Maxm=80
+// cutoff 1e-8 tstep 0.01 T=2 (N_t=201), full analytic Hessian with the rows
+// sharded over setThreadCount(G) shards (GPUs; on one device, concurrent
+// contexts), GRAPE controls U(2,10) and GROUP M=10 (chopped sine on a linear
+// seed, c ~ U(-2,2)).  G = 1 (and only G = 1 on the oracle) unless argv[3]
+// lists shard counts.
+static void scen_config3(Json& js, const std::vector<int>& shard_counts) {
+  srand_(3);
+  BoseHubbard sites(5, 4);
+  MPS ini = load_state(skey(5, 5, 5, 1.0, 2.5)), tgt = load_state(skey(5, 5, 5, 1.0, 50.0));
+  Stepper st(sites, 1.0, 0.01, Args(1e-8, 80));
+  const int N = 201, M = 10;
+  stdvec u0 = SeedGenerator::linspace(2.5, 50.0, N);
+  ControlBasis basis = ControlBasisFactory::buildChoppedSineBasis(u0, 0.01, 2.0, M);
+  const stdvec u = randseed(2, 10, N), c = randseed(-2, 2, M);
+  OC grape(tgt, ini, st, N, 1e-6), group(tgt, ini, st, basis, 1e-6);
+  for (int G : shard_counts) {
+    grape.setThreadCount(G);
+    group.setThreadCount(G);
+    js.mat("grape_G" + std::to_string(G), grape.getHessian(u));
+    js.mat("group_G" + std::to_string(G), group.getHessian(c));
+  }
+  js.vec("grape_grad", grape.getAnalyticGradient(u));
+  js.vec("group_grad", group.getAnalyticGradient(c));
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s <basis|cost|gradient|hessian|sequencing|golden|nlp> <state-dir>\n", argv[0]);
@@ -538,6 +564,15 @@ int main(int argc, char** argv) {
     else if (sc == "sequencing") scen_sequencing(js);
     else if (sc == "golden") scen_golden(js);
     else if (sc == "nlp") scen_nlp(js);
+    else if (sc == "config3") {
+      std::vector<int> gs;
+      if (argc > 3) {
+        std::stringstream ss(argv[3]);
+        for (std::string t; std::getline(ss, t, ',');) gs.push_back(std::stoi(t));
+      }
+      if (gs.empty()) gs.push_back(1);
+      scen_config3(js, gs);
+    }
     else throw std::runtime_error("unknown scenario " + sc);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "error: %s\n", e.what());

@@ -50,9 +50,9 @@ def write_states(directory):
             f.write(hdr.tobytes() + dims.tobytes() + data.tobytes())
 
 
-def run(kind, scenario, directory, timeout=1200):
+def run(kind, scenario, directory, timeout=1200, extra=()):
     exe = build_driver(kind)
-    r = subprocess.run([exe, scenario, directory], capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run([exe, scenario, directory, *extra], capture_output=True, text=True, timeout=timeout)
     if r.returncode != 0:
         raise RuntimeError(f"{kind} driver '{scenario}' failed: {r.stderr.strip()}")
     return json.loads(r.stdout)
