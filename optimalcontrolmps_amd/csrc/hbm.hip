@@ -235,8 +235,10 @@ struct Engine {
     for (int D = 0; D < 24; ++D) { gcst.glo[D] = glo[D]; gcst.gsz[D] = gsz[D]; gcst.goff[D] = goff[D]; }
     d_gf.reserve(gtotal);
     d_gb.reserve(gtotal);
-    HCK(hipMemcpy(d_gf.p, gf.data(), sizeof(z) * gtotal, hipMemcpyHostToDevice));
-    HCK(hipMemcpy(d_gb.p, gb.data(), sizeof(z) * gtotal, hipMemcpyHostToDevice));
+    sync();  // set_tstep: queued steps may still read the old gates
+    HCK(hipMemcpyAsync(d_gf.p, gf.data(), sizeof(z) * gtotal, hipMemcpyHostToDevice, st));
+    HCK(hipMemcpyAsync(d_gb.p, gb.data(), sizeof(z) * gtotal, hipMemcpyHostToDevice, st));
+    sync();
   }
   // per-bond capacities from max(Maxm, widest state seen), capped by the
   // Hilbert-space bound; chains and the state heap are sized from them

@@ -216,8 +216,9 @@ static int upload_gates(ocg_ctx* c) {
     HIPCHK(c, hipMalloc(&c->d_gf, sizeof(zc) * off));
     HIPCHK(c, hipMalloc(&c->d_gb, sizeof(zc) * off));
   }
-  HIPCHK(c, hipMemcpy(c->d_gf, gf.data(), sizeof(zc) * off, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_gb, gb.data(), sizeof(zc) * off, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpyAsync(c->d_gf, gf.data(), sizeof(zc) * off, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_gb, gb.data(), sizeof(zc) * off, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
 }
 
@@ -234,11 +235,18 @@ static int ensure_slots(ocg_ctx* c, int nslots) {
   zc* nx = nullptr;
   HIPCHK(c, hipMalloc(&nd, sizeof(int) * size_t(n) * c->P.nsq));
   HIPCHK(c, hipMalloc(&nx, sizeof(zc) * size_t(n) * c->P.cap));
-  HIPCHK(c, hipMemset(nd, 0, sizeof(int) * size_t(n) * c->P.nsq));
+  // every copy / fill is ordered on the context's (non-blocking) stream: a
+  // null-stream hipMemset / device-to-device hipMemcpy is asynchronous to the
+  // host and unordered with it, so a later upload or kernel could overtake it
+  HIPCHK(c, hipMemsetAsync(nd, 0, sizeof(int) * size_t(n) * c->P.nsq, c->stream));
   if (c->nslots) {
-    HIPCHK(c, hipMemcpy(nd, c->pool.dims, sizeof(int) * size_t(c->nslots) * c->P.nsq, hipMemcpyDeviceToDevice));
-    HIPCHK(c, hipMemcpy(nx, c->pool.data, sizeof(zc) * size_t(c->nslots) * c->P.cap,
-                        hipMemcpyDeviceToDevice));
+    HIPCHK(c, hipMemcpyAsync(nd, c->pool.dims, sizeof(int) * size_t(c->nslots) * c->P.nsq, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(nx, c->pool.data, sizeof(zc) * size_t(c->nslots) * c->P.cap, hipMemcpyDeviceToDevice,
+                             c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->nslots) {
     (void)hipFree(c->pool.dims);
     (void)hipFree(c->pool.data);
   }
@@ -251,6 +259,7 @@ static int ensure_slots(ocg_ctx* c, int nslots) {
 template <class T>
 static int ensure_buf(ocg_ctx* c, T*& ptr, int& cap, int n) {
   if (n <= cap) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // queued work may still read the old buffer
   if (ptr) (void)hipFree(ptr);
   ptr = nullptr;
   int m = std::max(n, 2 * cap);
@@ -339,9 +348,11 @@ static int begin_kernel(ocg_ctx* c) {
 // not be read as a valid psi_t / xi_t / xiH_t).
 static int check_err(ocg_ctx* c) {
   int err = 0;
-  HIPCHK(c, hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (!err) return 0;
-  HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
+  HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_psi = c->have_xi = c->have_xih = false;
   std::string m;
   if (err & OCG_ERR_JACOBI) m += "eigensolver did not converge within its sweep cap; ";
@@ -414,6 +425,19 @@ static int finish_params(ocg_ctx* c) {
   return 0;
 }
 
+
+// the context's stream and timing events (every copy, fill and launch of a
+// context is ordered on this one non-blocking stream)
+static bool make_stream(ocg_ctx* c) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->evh[0]) != hipSuccess || hipEventCreate(&c->evh[1]) != hipSuccess ||
+      hipEventCreate(&c->evh[2]) != hipSuccess || hipEventCreate(&c->evh[3]) != hipSuccess) {
+    c->err = "stream/event creation failed";
+    return false;
+  }
+  return true;
+}
 
 // forward an HBM-engine status (its message becomes the context's)
 static int hb(ocg_ctx* c, int rc) {
@@ -490,6 +514,7 @@ int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, d
   }
   if (device < 0 || device >= ndev) { c->err = "device index out of range"; return bail(OCG_EINVAL); }
   if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(OCG_EHIP); }
+  if (!make_stream(c)) return bail(OCG_EHIP);
   int rc = 0;
   if (engine != 2) {
     rc = build_params(c, L, p, npart, tstep, cutoff, maxm);
@@ -502,6 +527,10 @@ int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, d
       ocg_ctx* h = new ocg_ctx;
       h->device = device;
       h->J = J;
+      if (!make_stream(h)) {
+        ocg_destroy(h);
+        return bail(OCG_EHIP);
+      }
       std::swap(c, h);
       ocg_destroy(h);
       if ((rc = create_hbm(c, L, p, npart, tstep, cutoff, maxm))) return bail(rc);
@@ -511,22 +540,17 @@ int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, d
   } else if ((rc = create_hbm(c, L, p, npart, tstep, cutoff, maxm))) {
     return bail(rc);
   }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->evh[0]) != hipSuccess || hipEventCreate(&c->evh[1]) != hipSuccess ||
-      hipEventCreate(&c->evh[2]) != hipSuccess || hipEventCreate(&c->evh[3]) != hipSuccess) {
-    c->err = "stream/event creation failed";
-    return bail(OCG_EHIP);
-  }
   if (c->hbm) {
     *out = c;
     return 0;
   }
   if (hipMalloc(&c->d_md, sizeof(int) * c->md.size()) != hipSuccess ||
-      hipMemcpy(c->d_md, c->md.data(), sizeof(int) * c->md.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpyAsync(c->d_md, c->md.data(), sizeof(int) * c->md.size(), hipMemcpyHostToDevice, c->stream) !=
+          hipSuccess ||
       hipMalloc(&c->d_stats, sizeof(double) * 24) != hipSuccess ||
-      hipMemset(c->d_stats, 0, sizeof(double) * 24) != hipSuccess ||
-      hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess) {
+      hipMemsetAsync(c->d_stats, 0, sizeof(double) * 24, c->stream) != hipSuccess ||
+      hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
     c->err = "device allocation failed";
     return bail(OCG_EHIP);
   }
@@ -698,7 +722,8 @@ static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::ve
                      c->d_idx, c->d_idx + n, n, with_dH, c->d_c, c->d_stats + 1 * 3);
   if (int rc = end_kernel(c, 1)) return rc;
   out.resize(n);
-  HIPCHK(c, hipMemcpy(out.data(), c->d_c, sizeof(zc) * n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(out.data(), c->d_c, sizeof(zc) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
 }
 
@@ -730,7 +755,10 @@ static int launch_apply_dH(ocg_ctx* c, const std::vector<int>& in, const std::ve
   hipLaunchKernelGGL(k_apply_dH, dim3(n), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
                      c->d_idx, c->d_idx + n, n, norms ? c->d_norms : nullptr, c->d_stats + 2 * 3);
   if (int rc = end_kernel(c, 2)) return rc;
-  if (norms) HIPCHK(c, hipMemcpy(norms, c->d_norms, sizeof(double) * n, hipMemcpyDeviceToHost));
+  if (norms) {
+    HIPCHK(c, hipMemcpyAsync(norms, c->d_norms, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   return 0;
 }
 
@@ -875,9 +903,11 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
     if (int rc = end_kernel(c, 2)) return rc;
     // k_apply_dH writes norms[r] (row order); scatter to index i on the host side of the rows kernel
     std::vector<double> nr(nrows), ni(N, 0.0);
-    HIPCHK(c, hipMemcpy(nr.data(), c->d_rnorm, sizeof(double) * nrows, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpyAsync(nr.data(), c->d_rnorm, sizeof(double) * nrows, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int r = 0; r < nrows; ++r) ni[rows[r]] = nr[r];
-    HIPCHK(c, hipMemcpy(c->d_rnorm, ni.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpyAsync(c->d_rnorm, ni.data(), sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   zc f2 = mkz(F[0], F[1]);
   if (int rc = begin_kernel(c)) return rc;
@@ -886,7 +916,8 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
                      c->d_H, c->d_stats + 3 * 3);
   if (int rc = end_kernel(c, 3)) return rc;
   std::vector<double> h(hn);
-  HIPCHK(c, hipMemcpy(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   // entries of the requested rows and their mirrors (disjoint per row)
   for (int r = 0; r < nrows; ++r) {
     int i = rows[r];
@@ -937,7 +968,8 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     c->d_flags = nullptr;
     c->flags_cap = 0;
     if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N + 1)) return rc;
-    HIPCHK(c, hipMemset(c->d_flags, 0, sizeof(int) * c->flags_cap));
+    HIPCHK(c, hipMemsetAsync(c->d_flags, 0, sizeof(int) * c->flags_cap, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->epoch = 0;
   }
   // stored row states: row i keeps psiH_i(j), j = i..N-2 (O(N^2) states).
@@ -1046,7 +1078,8 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   }
   if (err) {
     c->have_psi = c->have_xi = c->have_xih = false;
-    HIPCHK(c, hipMemset(c->d_err, 0, sizeof(int)));
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return fail(c, OCG_ENUM, std::string((err & OCG_ERR_WATCHDOG) ? "pipeline watchdog: a consumer saw no producer "
                                                                     "progress for ~15 s; " : "") +
                                  ((err & OCG_ERR_JACOBI) ? "eigensolver did not converge within its sweep cap" : ""));
@@ -1090,7 +1123,8 @@ int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, dou
   }
   HIPCHK(c, hipSetDevice(c->device));
   double s[3];
-  HIPCHK(c, hipMemcpy(s, c->d_stats + 3 * kind, sizeof(s), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(s, c->d_stats + 3 * kind, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (total_ms) *total_ms = c->kst[kind].ms;
   if (launches) *launches = c->kst[kind].launches;
   if (alg_bytes) *alg_bytes = s[0];
@@ -1123,7 +1157,8 @@ int ocg_reset_stats(ocg_ctx* c) {
     return 0;
   }
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemset(c->d_stats, 0, sizeof(double) * 24));
+  HIPCHK(c, hipMemsetAsync(c->d_stats, 0, sizeof(double) * 24, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   for (auto& k : c->kst) k = KStat{};
   return 0;
 }

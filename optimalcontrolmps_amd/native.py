@@ -44,7 +44,7 @@ def build_native(force: bool = False, nt: int | None = None, verbose: bool = Fal
         flags.append(f"-DOCG_NT={int(nt)}")
     deps = {
         "ocmps": ["ocmps.hip", "engine.hpp", "engine_device.hpp", "kernels.hpp", "params.hpp", "hbm.hpp"],
-        "hbm": ["hbm.hip", "hbm.hpp", "hbm_device.hpp"],
+        "hbm": ["hbm.hip", "hbm.hpp", "hbm_device.hpp", "hbm_eig.hpp"],
     }
     tag = f"nt{int(nt)}" if nt else "prod"
     objs, procs = [], []
