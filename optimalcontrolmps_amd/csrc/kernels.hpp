@@ -147,9 +147,12 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
 //                [2+nxw, 2+nxw+nrows) row r: wait psi_i, psiH = dH psi_i, store
 //                psiH_i(i..N-2) (the states calcHessianRow overlaps, :251-279)
 //   k_row_overlaps  one workgroup per stored psiH_i(j): overlap with xiH_j, H_ij
-// Producers and consumers live in one grid; consumers only ever wait on
-// blocks 0 and 1, which are dispatched first, so progress does not depend on
-// co-residency.  Every publication also bumps a progress counter
+// Producers and consumers live in one grid.  Roles are taken by ticket (the
+// order in which workgroups start running, flags[2N+1], zeroed per launch),
+// not by blockIdx: every role only ever waits on roles with lower tickets,
+// which are already running, so progress holds whatever the dispatch order
+// and however few workgroups fit the device (long horizons: N_t = 801 has
+// 799 rows > CUs).  Every publication also bumps a progress counter
 // (flags[2N]); a waiter gives up (err |= OCG_ERR_WATCHDOG) only after ~2^24
 // polls (~15 s) during which no producer published anything, so a slow but
 // live pipeline (long horizons, large chains, several shards per GPU) never
@@ -198,8 +201,12 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
                                          const int* rbase, Pool rs, double* rnorm, int* flags, int epoch, int* err,
                                          int nxw, double* stats) {
   Chain<NT> c(P, smem);
+  if (threadIdx.x == 0)
+    c.ISCAL[14] = __hip_atomic_fetch_add(flags + 2 * N + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int b = c.ISCAL[14];  // this workgroup's role
+  __syncthreads();
   c.load_tables(gf, gb, md);
-  const int b = blockIdx.x;
   int* const progress = flags + 2 * N;
   double bytes = 0, flops = 0, nsteps = 0;
   if (b < 2) {

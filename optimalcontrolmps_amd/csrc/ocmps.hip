@@ -963,11 +963,11 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   if (int rc = ensure_buf(c, c->d_pc, c->pc_cap, N + 1)) return rc;
   if (int rc = ensure_buf(c, c->d_rows, c->rows_cap, 2 * nrows + 2)) return rc;
   if (int rc = ensure_buf(c, c->d_prn, c->prn_cap, nrows + 1)) return rc;
-  if (2 * N + 1 > c->flags_cap) {  // publication flags (+ progress counter) start at 0 (< any epoch)
+  if (2 * N + 2 > c->flags_cap) {  // publication flags (+ progress counter) start at 0 (< any epoch)
     if (c->d_flags) (void)hipFree(c->d_flags);
     c->d_flags = nullptr;
     c->flags_cap = 0;
-    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N + 1)) return rc;
+    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N + 2)) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_flags, 0, sizeof(int) * c->flags_cap, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->epoch = 0;
@@ -1014,6 +1014,7 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   HIPCHK(c, hipMemcpyAsync(c->d_rows, rb.data(), sizeof(int) * rb.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_flags + 2 * N + 1, 0, sizeof(int), c->stream));  // role tickets
   const int* d_rows = c->d_rows;
   const int* d_rbase = c->d_rows + nrows;
   // divT_i = <xi_i|dH|psi_i> and F = <psi_{N-1}|target> pair lists

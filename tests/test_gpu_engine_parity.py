@@ -272,3 +272,46 @@ def test_maxm_binding_vs_oracle(states, maxm):
     Ho = oc.hessian(u, 4)
     assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
     assert np.abs(0.01 * (divT * F * 1j).real - oc.gradient(u)).max() < 1e-6
+
+
+def _with_env(name, value, fn):
+    import os
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ[name]
+        else:
+            os.environ[name] = old
+
+
+def test_fused_equals_unfused_config1_full_horizon(states):
+    """config 1 at its full N_t = 201: the fused pipeline (ticket roles, rows
+    overlapped with the trajectories) equals the two-phase path bit for bit"""
+    L, p, N, J = 5, 5, 5, 1.0
+    u = np.random.default_rng(23).uniform(2, 10, 201)
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    eng.set_states(tgt, ini)
+    H1, d1, F1 = eng.hessian(u)
+    divT, F, fid, H2 = run_engine_hessian(eng, u, tgt, ini)
+    assert np.array_equal(d1, divT) and F1 == F
+    assert np.array_equal(H1, H2)
+
+
+def test_long_horizon_rows_exceed_cus(states):
+    """N_t = 801 (T = 8 at config 1's dt): 799 Hessian rows, more workgroups
+    than the device has CUs.  Roles are taken by ticket, so the pipeline makes
+    progress whatever the dispatch order; it must equal the unfused path."""
+    L, p, N, J = 5, 5, 5, 1.0
+    u = np.random.default_rng(801).uniform(2, 10, 801)
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    eng.set_states(tgt, ini)
+    H1, d1, F1 = eng.hessian(u)
+    divT, F, fid, H2 = run_engine_hessian(eng, u, tgt, ini)
+    assert np.array_equal(d1, divT) and F1 == F
+    assert np.array_equal(H1, H2)
+    assert np.isfinite(H1).all() and np.abs(H1).max() > 0
