@@ -145,6 +145,13 @@ int ocg_hessian(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows
  * ocg_steps returns are in the reference's gauge. */
 int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
 
+/* ControlBasis::convertHessian (src/ControlBasis.cpp:91-116) on the device:
+ * Hc (M x M) = V Hu V^T with Hu row-major N x N (host), V row-major M x N
+ * (V[n][i] = S_i f_{i n}, the transposed control Jacobian).  Each entry is a
+ * sequential inner product in the reference's order without fused
+ * multiply-adds: bit-identical to the host restatement.  Any engine. */
+int ocg_convert_hessian(ocg_ctx* ctx, const double* Hu, int N, const double* V, int M, double* Hc);
+
 /* ------------------------------------------------------ instrumentation
  * Per-kernel HIP-event timing on the context's stream and the algorithmic
  * traffic model of DESIGN.md §Roofline.  kind: 0 trajectory, 1 overlaps,

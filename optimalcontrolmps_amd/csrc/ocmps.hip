@@ -105,6 +105,39 @@ __global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const z
   ocg::body_steps<NT>(smem, P, gf, gb, md, pool, slots, n, u, u_stride, nsteps, forward, stats);
 }
 
+// ControlBasis::convertHessian (src/ControlBasis.cpp:91-116): H_c = V H_u V^T,
+// V_{n i} = S_i f_{i n}.  Every entry is one sequential inner product in the
+// reference's order (std::inner_product: acc = acc + a * b, no fused
+// multiply-add), so the device result is bit-identical to the host facade's.
+// Stage 1, one workgroup per row k of H_u (row staged in LDS), one thread per
+// basis vector j: HV[j][k] = sum_l H_u[k][l] V[j][l] (V read transposed,
+// coalesced over j).  Stage 2, one thread per (i, j >= i):
+// H_c[i][j] = H_c[j][i] = sum_k V[i][k] HV[j][k].
+__global__ __launch_bounds__(256) void k_project_hv(const double* Hu, const double* Vt, int N, int M, double* HV) {
+#pragma clang fp contract(off)
+  extern __shared__ __align__(16) char smem[];
+  double* row = (double*)smem;
+  const int k = blockIdx.x;
+  for (int l = threadIdx.x; l < N; l += blockDim.x) row[l] = Hu[(size_t)k * N + l];
+  __syncthreads();
+  for (int j = threadIdx.x; j < M; j += blockDim.x) {
+    double acc = 0.0;
+    for (int l = 0; l < N; ++l) acc = acc + row[l] * Vt[(size_t)l * M + j];
+    HV[(size_t)j * N + k] = acc;
+  }
+}
+__global__ __launch_bounds__(256) void k_project_c(const double* V, const double* HV, int N, int M, double* Hc) {
+#pragma clang fp contract(off)
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * M) return;
+  const int i = t / M, j = t % M;
+  if (j < i) return;
+  double acc = 0.0;
+  for (int k = 0; k < N; ++k) acc = acc + V[(size_t)i * N + k] * HV[(size_t)j * N + k];
+  Hc[(size_t)i * M + j] = acc;
+  Hc[(size_t)j * M + i] = acc;
+}
+
 // ==========================================================================
 // host side
 // ==========================================================================
@@ -176,12 +209,15 @@ struct ocg_ctx {
   int* d_err = nullptr;
   int* d_rows = nullptr;      // rows, then rbase (nrows + 1)
   int rows_cap = 0;
+  double* d_proj = nullptr;   // convertHessian operands (H_u, V, V^T, HV, H_c)
+  size_t proj_cap = 0;
   zc* d_pc = nullptr;         // divT (N) and F (1) on the device
   int pc_cap = 0;
   double* d_prn = nullptr;    // psiH norms by row slot
   int prn_cap = 0;
   // trajectory state
   int N = 0;
+  std::vector<double> u_psi, u_xi;  // controls of the device psi_t / xi_t (empty: none)
   bool have_states = false, have_psi = false, have_xi = false, have_xih = false;
   KStat kst[8];
   // slot map
@@ -439,6 +475,17 @@ static bool make_stream(ocg_ctx* c) {
   return true;
 }
 
+// controls of the device trajectories, so a Hessian at the control of the
+// last gradient reuses psi_t / xi_t / xiHlist (BH_nlp::eval_h after
+// eval_grad_f, src/BH_nlp.cpp:189)
+static void note_u(ocg_ctx* c, const double* u, int N, int which) {
+  if (which & 1) c->u_psi.assign(u, u + N);
+  if (which & 2) c->u_xi.assign(u, u + N);
+}
+static bool same_u(const std::vector<double>& a, const double* u, int N) {
+  return a.size() == size_t(N) && std::memcmp(a.data(), u, sizeof(double) * N) == 0;
+}
+
 // forward an HBM-engine status (its message becomes the context's)
 static int hb(ocg_ctx* c, int rc) {
   if (rc) c->err = hbm_last_error(c->hbm);
@@ -582,6 +629,7 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->d_rows) (void)hipFree(c->d_rows);
   if (c->d_pc) (void)hipFree(c->d_pc);
   if (c->d_prn) (void)hipFree(c->d_prn);
+  if (c->d_proj) (void)hipFree(c->d_proj);
   if (c->d_idx) (void)hipFree(c->d_idx);
   if (c->d_u) (void)hipFree(c->d_u);
   if (c->d_c) (void)hipFree(c->d_c);
@@ -621,6 +669,8 @@ int ocg_set_tstep(ocg_ctx* c, double tstep) {
   HIPCHK(c, hipSetDevice(c->device));
   c->P.dt = tstep;
   c->have_psi = c->have_xi = c->have_xih = false;
+  c->u_psi.clear();  // trajectories of the old dt are never reused
+  c->u_xi.clear();
   if (c->hbm) {
     OcgParams G{};
     G.p = c->P.p;
@@ -777,6 +827,8 @@ int ocg_apply_dH(ocg_ctx* c, const int* dims, const double* data, int* out_dims,
 int ocg_set_states(ocg_ctx* c, const int* dims_target, const double* target, const int* dims_init,
                    const double* init) {
   if (!c || !dims_target || !target || !dims_init || !init) return c ? fail(c, OCG_EINVAL, "null argument") : OCG_EINVAL;
+  c->u_psi.clear();
+  c->u_xi.clear();
   if (c->hbm) return hb(c, hbm_set_states(c->hbm, dims_target, target, dims_init, init));
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = upload_mps(c, c->slot_target(), dims_target, target)) return rc;
@@ -788,7 +840,13 @@ int ocg_set_states(ocg_ctx* c, const int* dims_target, const double* target, con
 
 int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
   if (!c || !u || N < 2 || which < 1 || which > 3) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
-  if (c->hbm) return hb(c, hbm_propagate(c->hbm, u, N, which));
+  if (which & 1) c->u_psi.clear();
+  if (which & 2) c->u_xi.clear();
+  if (c->hbm) {
+    const int rc = hb(c, hbm_propagate(c->hbm, u, N, which));
+    if (!rc) note_u(c, u, N, which);
+    return rc;
+  }
   if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
   HIPCHK(c, hipSetDevice(c->device));
   const OcgParams& P = c->P;
@@ -807,6 +865,7 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
   if (int rc = end_kernel(c, 0)) return rc;
   if (which & 1) { c->have_psi = true; c->have_xih = c->have_xih && (which & 2); }
   if (which & 2) { c->have_xi = true; c->have_xih = false; }
+  note_u(c, u, N, which);
   return 0;
 }
 
@@ -931,12 +990,22 @@ int ocg_hessian_rows(ocg_ctx* c, const double* u, int N, const int* rows, int nr
 
 // getHessian's fidelity part from the separate entry points (calcPsiXiDivT,
 // xiHlist, calcHessianRow over all rows: src/OptimalControl.cpp:281-338)
+// When the device psi_t / xi_t already belong to u (a Hessian at the control
+// of the last gradient: BH_nlp::eval_h after eval_grad_f, src/BH_nlp.cpp:189,
+// whose getHessian always passes new_control = true) they, and xiHlist if
+// present, are reused: the same states, so the same Hessian bit for bit.
 static int hessian_unfused(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                            double* F) {
-  if (int rc = ocg_propagate(c, u, N, 3)) return rc;
+  const bool have_psi = c->hbm ? hbm_have(c->hbm, 1) : c->have_psi;
+  const bool have_xi = c->hbm ? hbm_have(c->hbm, 2) : c->have_xi;
+  const bool reuse = have_psi && have_xi && same_u(c->u_psi, u, N) && same_u(c->u_xi, u, N);
+  if (!reuse)
+    if (int rc = ocg_propagate(c, u, N, 3)) return rc;
   if (int rc = ocg_div_t(c, divT)) return rc;
   if (int rc = ocg_overlap_factor(c, F)) return rc;
-  if (int rc = ocg_xi_dH(c)) return rc;
+  const bool have_xih = c->hbm ? hbm_have(c->hbm, 3) : c->have_xih;
+  if (!(reuse && have_xih))
+    if (int rc = ocg_xi_dH(c)) return rc;
   return ocg_hessian_rows(c, u, N, rows, nrows, F, divT, H);
 }
 
@@ -1086,6 +1155,7 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
                                  ((err & OCG_ERR_JACOBI) ? "eigensolver did not converge within its sweep cap" : ""));
   }
   c->have_psi = c->have_xi = c->have_xih = true;
+  note_u(c, u, N, 3);
   for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
   F[0] = pc[N].x;
   F[1] = pc[N].y;
@@ -1096,6 +1166,34 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
       H[size_t(j) * N + i] = h[size_t(j) * N + i];
     }
   }
+  return 0;
+}
+
+int ocg_convert_hessian(ocg_ctx* c, const double* Hu, int N, const double* V, int M, double* Hc) {
+  if (!c || !Hu || !V || !Hc || N < 1 || M < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t nn = size_t(N) * N, mn = size_t(M) * N, need = nn + 3 * mn + size_t(M) * M;
+  if (need > c->proj_cap) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->d_proj) (void)hipFree(c->d_proj);
+    c->d_proj = nullptr;
+    c->proj_cap = 0;
+    HIPCHK(c, hipMalloc(&c->d_proj, sizeof(double) * need));
+    c->proj_cap = need;
+  }
+  double *dH = c->d_proj, *dV = dH + nn, *dVt = dV + mn, *dHV = dVt + mn, *dHc = dHV + mn;
+  std::vector<double> vt(mn);
+  for (int j = 0; j < M; ++j)
+    for (int l = 0; l < N; ++l) vt[size_t(l) * M + j] = V[size_t(j) * N + l];
+  HIPCHK(c, hipMemcpyAsync(dH, Hu, sizeof(double) * nn, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dV, V, sizeof(double) * mn, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dVt, vt.data(), sizeof(double) * mn, hipMemcpyHostToDevice, c->stream));
+  const int bt = std::min(256, ((M + 63) / 64) * 64);
+  hipLaunchKernelGGL(k_project_hv, dim3(N), dim3(bt), sizeof(double) * N, c->stream, dH, dVt, N, M, dHV);
+  hipLaunchKernelGGL(k_project_c, dim3((M * M + 255) / 256), dim3(256), 0, c->stream, dV, dHV, N, M, dHc);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(Hc, dHc, sizeof(double) * M * M, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
 }
 

@@ -85,6 +85,9 @@ class ControlBasis {
   }
 
   rowmat getControlJacobian() const { return jac; }
+  // V (M x N), V[n][i] = S_i f_{i n}: the operand of device projections
+  // (GpuTDMRG::Engine::convertHessian, ocg_convert_hessian)
+  const rowmat& basisMatrix() const { return V; }
 
  private:
   stdvec u0, S;

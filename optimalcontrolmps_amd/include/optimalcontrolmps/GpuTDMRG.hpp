@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../../include/ocmps.h"
+#include "ControlBasis.hpp"
 #include "MPS.hpp"
 
 namespace ocmps {
@@ -252,6 +253,21 @@ class GpuTDMRG::Engine {
     dT.resize(N);
     for (size_t i = 0; i < N; ++i) dT[i] = Cplx(dv[2 * i], dv[2 * i + 1]);
     gather_rows(rows, part, H);
+  }
+  // ControlBasis::convertHessian (src/ControlBasis.cpp:91-116) on shard 0's
+  // device: bit-identical to the host restatement (ocg_convert_hessian)
+  rowmat convertHessian(const ControlBasis& basis, const rowmat& Hu) {
+    const rowmat& V = basis.basisMatrix();
+    const size_t M = V.size(), n = Hu.size();
+    if (M == 0 || n != N) return basis.convertHessian(Hu);
+    std::vector<double> h(n * n), v(M * n), hc(M * M);
+    for (size_t i = 0; i < n; ++i) std::copy(Hu[i].begin(), Hu[i].end(), h.begin() + i * n);
+    for (size_t j = 0; j < M; ++j) std::copy(V[j].begin(), V[j].end(), v.begin() + j * n);
+    ocg_ctx* c = shards[0].get();
+    detail::check(ocg_convert_hessian(c, h.data(), int(n), v.data(), int(M), hc.data()), c, "ocg_convert_hessian");
+    rowmat Hc(M, stdvec(M));
+    for (size_t i = 0; i < M; ++i) std::copy(hc.begin() + i * M, hc.begin() + (i + 1) * M, Hc[i].begin());
+    return Hc;
   }
   std::vector<MPS> psiTrajectory() {
     std::vector<MPS> out;

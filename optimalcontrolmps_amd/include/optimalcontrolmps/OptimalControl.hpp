@@ -11,7 +11,8 @@
 //   std::unique_ptr<Engine> makeEngine(const MPS& target, const MPS& init, size_t N) const;
 //   Engine: setShards(n), propagate(u, which), divT(), overlapFactor(),
 //           fidelities(), precomputeXiH(), hessianRows(u, F, divT, H),
-//           hessianFresh(u, F&, divT&, H) (all of the above for a new control), psiTrajectory().
+//           hessianFresh(u, F&, divT&, H) (all of the above for a new control), psiTrajectory(),
+//           convertHessian(basis, Hu) (ControlBasis::convertHessian, src/ControlBasis.cpp:91-116).
 //
 // Host-side arithmetic kept verbatim from the reference: the regularisation
 // terms (:88-143), the gradient assembly g_i = dt Re(divT_i F i) (:240-246),
@@ -91,7 +92,8 @@ class OptimalControl {
   // one code path for any threadCount: the rows are sharded by the engine
   rowmat getHessian(const stdvec& control, const bool new_control = true) {
     if (GRAPE) return calcHessian(control, new_control);
-    return basis.convertHessian(calcHessian(basis.convertControl(control, new_control), new_control));
+    // ControlBasis::convertHessian by the engine (the GPU engine projects on the device)
+    return engine->convertHessian(basis, calcHessian(basis.convertControl(control, new_control), new_control));
   }
   stdvec getFidelityForAllT(const stdvec& control, const bool new_control = true) {
     return GRAPE ? calcFidelityForAllT(control, new_control)

@@ -109,6 +109,7 @@ SIGNATURES = [
     ("ocg_hessian_rows", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_hessian", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_convert_hessian", C.c_int, [C.c_void_p, dp, C.c_int, dp, C.c_int, dp]),
     ("ocg_kernel_stats", C.c_int, [C.c_void_p, C.c_int, dp, C.POINTER(C.c_long), dp, dp, C.POINTER(C.c_long)]),
     ("ocg_reset_stats", C.c_int, [C.c_void_p]),
     ("ocg_profile", C.c_int, [C.c_void_p, dp, C.c_int]),
@@ -315,6 +316,15 @@ class Engine:
         self._chk(lib().ocg_hessian(self.h, pu, N, pr, len(r), H.ctypes.data_as(dp), dv.ctypes.data_as(dp),
                                     Fa.ctypes.data_as(dp)), "ocg_hessian")
         return H, dv.view(np.complex128).copy(), complex(Fa[0], Fa[1])
+
+    def convert_hessian(self, Hu, V):
+        """ControlBasis::convertHessian on the device: V Hu V^T (V is M x N)"""
+        H, ph = _d(Hu)
+        Vm, pv = _d(V)
+        M, N = Vm.shape
+        out = np.zeros((M, M))
+        self._chk(lib().ocg_convert_hessian(self.h, ph, N, pv, M, out.ctypes.data_as(dp)), "ocg_convert_hessian")
+        return out
 
     def state(self, which, t) -> MPS:
         fd, d, n = self._out()

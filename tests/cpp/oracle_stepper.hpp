@@ -8,6 +8,7 @@
 #include <thread>
 
 #include "../../oracle/tdmrg_oracle.hpp"
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/ControlBasis.hpp"
 #include "../../optimalcontrolmps_amd/include/optimalcontrolmps/MPS.hpp"
 
 namespace ocmps_test {
@@ -89,6 +90,7 @@ class OracleTDMRG::Engine {
     precomputeXiH();
     hessianRows(u, F, dT, H);
   }
+  rowmat convertHessian(const ControlBasis& basis, const rowmat& Hu) { return basis.convertHessian(Hu); }
   std::vector<MPS> psiTrajectory() {
     std::vector<MPS> out;
     for (auto& m : oc.psi_t) out.push_back(from_oracle(m));
