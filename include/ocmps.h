@@ -94,6 +94,15 @@ int ocg_steps(ocg_ctx* ctx, const int* dims, const double* data, const double* u
 int ocg_step_batch(ocg_ctx* ctx, int n, const int* dims, const double* const* data, const double* u_from,
                    const double* u_to, int forward, int* out_dims, double* const* out_data, const size_t* out_cap,
                    size_t* out_nelem);
+/* Ground-state preparation on the device (replaces ITensor DMRG in
+ * InitializeState, include/InitializeState.hpp:18-117): nsteps imaginary-time
+ * Trotter steps exp(-tau H_BH(J, U)) of the state, the sweep of
+ * BH_tDMRG::step with exp(-tau h) gates and exp(-tau U n(n-1)/4) phases,
+ * normalised, truncated with the context's Cutoff/Maxm.  The context's
+ * real-time gates and device trajectories are left as they were.  The C++
+ * facade's InitializeState runs a tau schedule over this. */
+int ocg_imag_steps(ocg_ctx* ctx, const int* dims, const double* data, double U, double tau, int nsteps,
+                   int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem);
 /* overlapC(x, y) = <x|y> (with_dH = 0) or overlapC(x, propDeriv, y) = <x|dH|y>
  * (with_dH = 1) (src/OptimalControl.cpp:242, :412); out = {re, im} */
 int ocg_overlap(ocg_ctx* ctx, const int* dims_x, const double* x, const int* dims_y, const double* y,

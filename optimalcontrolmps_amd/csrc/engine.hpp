@@ -39,6 +39,7 @@ struct OcgParams {
   int th2cap;               // two-site Θ elements bound (physical bonds)
   int nplan;                // decomposition plan slots in LDS (0: plans off)
   int plan_pe;              // Θ elements a plan slot can describe
+  int imag;                 // 1: imaginary-time steps exp(-dt H) (ground-state preparation), 0: exp(-i dt H)
   int* err;                 // device error word of the context (bit 0: Jacobi sweep cap
                             // reached, bit 1: pipeline watchdog); checked after every launch
 };

@@ -2167,13 +2167,19 @@ struct Chain {
       zc f;
       if (ufrom == ph_u && forward == ph_dir) {
         f = PH[p + tid];
+      } else if (P.imag) {
+        f = c2(exp(-0.25 * ufrom * tau * nn), 0.0);  // exp(-tau U/4 n(n-1)): imaginary time
       } else {
         sincos(-0.25 * ufrom * tau * nn, &s, &c);
         f = c2(c, s);
       }
-      sincos(-0.25 * uto * tau * nn, &s, &c);
       PH[tid] = f;
-      PH[p + tid] = c2(c, s);
+      if (P.imag) {
+        PH[p + tid] = c2(exp(-0.25 * uto * tau * nn), 0.0);
+      } else {
+        sincos(-0.25 * uto * tau * nn, &s, &c);
+        PH[p + tid] = c2(c, s);
+      }
     }
     ph_u = uto;
     ph_dir = forward;

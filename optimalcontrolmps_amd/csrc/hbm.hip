@@ -921,7 +921,7 @@ struct Engine {
           z* b = cs[i]->site(k) + o;
           CTask c = ctask(b, b, d(k - 1, q), ld, ld, ld);
           const double a = -0.25 * u[i] * tau[i] * n * (n - 1);
-          c.f = mk(std::cos(a), std::sin(a));
+          c.f = gcst.imag ? mk(std::exp(a), 0.0) : mk(std::cos(a), std::sin(a));
           if (inv_norm) c.f = mk(c.f.x * (*inv_norm)[i], c.f.y * (*inv_norm)[i]);
           ct.push_back(c);
         }
@@ -1573,6 +1573,15 @@ int hbm_set_tstep(hbm_engine* h, double tstep, const std::vector<double>& gf, co
     h->E->dt = tstep;
     h->E->set_gates(gf, gb, glo, gsz, goff, gtotal);
     h->have_psi = h->have_xi = h->have_xih = false;
+  });
+}
+
+int hbm_swap_gates(hbm_engine* h, int imag, double tstep, const std::vector<double>& gf,
+                   const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal) {
+  return guard(h, [&] {
+    h->E->dt = tstep;
+    h->E->set_gates(gf, gb, glo, gsz, goff, gtotal);
+    h->E->gcst.imag = imag;
   });
 }
 

@@ -19,6 +19,10 @@ const char* hbm_last_error(const hbm_engine* h);
 size_t hbm_mps_max_nelem(const hbm_engine* h);
 int hbm_set_tstep(hbm_engine* h, double tstep, const std::vector<double>& gf, const std::vector<double>& gb,
                   const int* glo, const int* gsz, const int* goff, int gtotal);
+// swap the step's gates and time mode (imag: exp(-dt H)) without touching the
+// device trajectories (ocg_imag_steps switches in and back out)
+int hbm_swap_gates(hbm_engine* h, int imag, double tstep, const std::vector<double>& gf,
+                   const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal);
 // n states (dims[i], data[i]) take nsteps steps each, controls u[i*u_stride + s]
 int hbm_steps(hbm_engine* h, int n, const int* dims, const double* const* data, const double* u, int u_stride,
               int nsteps, const int* fwd, int* out_dims, double* const* out_data, const size_t* out_cap,

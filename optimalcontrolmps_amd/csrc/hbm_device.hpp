@@ -226,9 +226,12 @@ struct GateTask {
 };
 struct GateConst {
   int p, Q1, glo[24], gsz[24], goff[24];
+  int imag;  // imaginary-time steps (ground-state preparation)
 };
-// exp(-i 0.25 u tau n (n-1)) (BH_tDMRG::initUGates, src/BH_tDMRG.cpp:83-87)
-__device__ __forceinline__ z uphase(double u, double tau, int n) {
+// exp(-i 0.25 u tau n (n-1)) (BH_tDMRG::initUGates, src/BH_tDMRG.cpp:83-87);
+// imaginary time: exp(-0.25 u tau n (n-1))
+__device__ __forceinline__ z uphase(double u, double tau, int n, int imag) {
+  if (imag) return mk(exp(-0.25 * u * tau * double(n * (n - 1))), 0.0);
   double s, c;
   sincos(-0.25 * u * tau * double(n * (n - 1)), &s, &c);
   return mk(c, s);
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(NT) void k_gate(const GateTask* __restrict__ tasks,
       if (r0 < 0 || c0 < 0) { addr[y] = ~size_t(0); v[y] = mk(0, 0); continue; }
       addr[y] = (size_t)thoff[q] + (size_t)(r0 + a) * tC[q] + c0 + c;
       z t = C.th[addr[y]];
-      if (C.mode == 0) t = zmul(t, zmul(uphase(C.uf, C.tau, n1), uphase(C.uf, C.tau, n2)));
+      if (C.mode == 0) t = zmul(t, zmul(uphase(C.uf, C.tau, n1, gc.imag), uphase(C.uf, C.tau, n2, gc.imag)));
       v[y] = t;
     }
     const z* G = (C.fwd ? gf : gb) + gc.goff[D];
@@ -265,8 +268,8 @@ __global__ __launch_bounds__(NT) void k_gate(const GateTask* __restrict__ tasks,
       z s = mk(0, 0);
       for (int xx = 0; xx < sz; ++xx) s = zadd(s, zmul(G[y * sz + xx], v[xx]));
       const int n1 = lo + y, n2 = D - n1;
-      if (C.mode == 1) s = zmul(s, zmul(uphase(C.ut, C.tau, n1), uphase(C.ut, C.tau, n2)));
-      else if (C.lonely) s = zmul(s, uphase(C.ut, C.tau, n2));
+      if (C.mode == 1) s = zmul(s, zmul(uphase(C.ut, C.tau, n1, gc.imag), uphase(C.ut, C.tau, n2, gc.imag)));
+      else if (C.lonely) s = zmul(s, uphase(C.ut, C.tau, n2, gc.imag));
       w[y] = s;
     }
     for (int y = 0; y < sz; ++y)

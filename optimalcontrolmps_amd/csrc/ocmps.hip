@@ -716,6 +716,45 @@ int ocg_step(ocg_ctx* c, const int* dims, const double* data, double from, doubl
   return ocg_steps(c, dims, data, u, 1, forward, out_dims, out_data, out_cap, out_nelem);
 }
 
+// Ground-state preparation (InitializeState, include/InitializeState.hpp:18-117):
+// nsteps imaginary-time Trotter steps exp(-tau H) at constant U, the same
+// sweep as BH_tDMRG::step with the gates and phases of imaginary time
+// (doStep normalises after every gate and at the end).  The context's real-
+// time gates are swapped back afterwards; device trajectories stay valid.
+int ocg_imag_steps(ocg_ctx* c, const int* dims, const double* data, double U, double tau, int nsteps,
+                   int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem) {
+  if (!c || !dims || !data || !out_dims || !out_data || nsteps < 0 || !(tau > 0))
+    return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const double dt0 = c->P.dt;
+  std::vector<double> u(size_t(nsteps) + 1, U);
+  int rc = 0;
+  if (c->hbm) {
+    OcgParams G{};
+    G.p = c->P.p;
+    G.dt = tau;
+    G.imag = 1;
+    std::vector<double> gf, gb;
+    ocg_host::gate_tables(G, c->J, gf, gb);
+    rc = hb(c, hbm_swap_gates(c->hbm, 1, tau, gf, gb, G.glo, G.gsz, G.goff, G.gtotal));
+    if (!rc) rc = ocg_steps(c, dims, data, u.data(), nsteps, 1, out_dims, out_data, out_cap, out_nelem);
+    G.dt = dt0;
+    G.imag = 0;
+    ocg_host::gate_tables(G, c->J, gf, gb);
+    const int rc2 = hbm_swap_gates(c->hbm, 0, dt0, gf, gb, G.glo, G.gsz, G.goff, G.gtotal);
+    if (!rc && rc2) rc = hb(c, rc2);
+    return rc;
+  }
+  c->P.dt = tau;
+  c->P.imag = 1;
+  rc = upload_gates(c);
+  if (!rc) rc = ocg_steps(c, dims, data, u.data(), nsteps, 1, out_dims, out_data, out_cap, out_nelem);
+  c->P.dt = dt0;
+  c->P.imag = 0;
+  const int rc2 = upload_gates(c);
+  return rc ? rc : rc2;
+}
+
 int ocg_step_batch(ocg_ctx* c, int n, const int* dims, const double* const* data, const double* u_from,
                    const double* u_to, int forward, int* out_dims, double* const* out_data, const size_t* out_cap,
                    size_t* out_nelem) {

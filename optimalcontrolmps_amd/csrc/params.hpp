@@ -32,7 +32,8 @@ inline long long hs_count(int m, int p, int q) {
 // exp(-i tau h), h = -J (a_1 a^dag_2 + a^dag_1 a_2) on (n1, n2) (p^2 x p^2,
 // row = out index n1'*p+n2'), summed by Horner like ITensor's
 // BondGate(tReal) Taylor series (reference src/BH_tDMRG.cpp:31-36), 60 orders.
-inline std::vector<std::complex<double>> hopping_gate(int p, double J, double tau) {
+// imag: exp(-tau h) instead (ITensor's BondGate(tImag); ground-state preparation).
+inline std::vector<std::complex<double>> hopping_gate(int p, double J, double tau, bool imag = false) {
   int D = p * p;
   std::vector<std::complex<double>> x(size_t(D) * D, 0.0), G(size_t(D) * D, 0.0), T(size_t(D) * D);
   for (int n1 = 0; n1 < p; ++n1)
@@ -41,7 +42,7 @@ inline std::vector<std::complex<double>> hopping_gate(int p, double J, double ta
       if (n1 >= 1 && n2 + 1 < p) x[size_t((n1 - 1) * p + n2 + 1) * D + in] += -J * std::sqrt(double(n1) * (n2 + 1));
       if (n2 >= 1 && n1 + 1 < p) x[size_t((n1 + 1) * p + n2 - 1) * D + in] += -J * std::sqrt(double(n1 + 1) * n2);
     }
-  for (auto& v : x) v *= std::complex<double>(0, -tau);
+  for (auto& v : x) v *= imag ? std::complex<double>(-tau, 0) : std::complex<double>(0, -tau);
   for (int i = 0; i < D; ++i) G[size_t(i) * D + i] = 1.0;
   for (int ord = 60; ord >= 1; --ord) {
     for (int i = 0; i < D; ++i)
@@ -58,7 +59,7 @@ inline std::vector<std::complex<double>> hopping_gate(int p, double J, double ta
 // per-Δ (= n1 + n2) blocks of the forward/backward gates; fills P.glo/gsz/goff/gtotal
 inline void gate_tables(OcgParams& P, double J, std::vector<double>& gf, std::vector<double>& gb) {
   const int p = P.p;
-  auto Gf = hopping_gate(p, J, P.dt), Gb = hopping_gate(p, J, -P.dt);
+  auto Gf = hopping_gate(p, J, P.dt, P.imag != 0), Gb = hopping_gate(p, J, -P.dt, P.imag != 0);
   gf.clear();
   gb.clear();
   int off = 0;

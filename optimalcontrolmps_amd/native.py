@@ -96,6 +96,7 @@ SIGNATURES = [
     ("ocg_mps_nelem", C.c_size_t, [C.c_int, C.c_int, C.c_int, ip]),
     ("ocg_step", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_steps", C.c_int, [C.c_void_p, ip, dp, dp, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_imag_steps", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_step_batch", C.c_int, [C.c_void_p, C.c_int, ip, C.POINTER(dp), dp, dp, C.c_int, ip, C.POINTER(dp), szp,
                                  szp]),
     ("ocg_overlap", C.c_int, [C.c_void_p, ip, dp, ip, dp, C.c_int, dp]),
@@ -219,6 +220,15 @@ class Engine:
         uu, pu = _d(u)
         self._chk(lib().ocg_steps(self.h, pd, pr, pu, len(uu) - 1, int(forward), fd.ctypes.data_as(ip),
                                   d.ctypes.data_as(dp), self.cap, C.byref(n)), "ocg_steps")
+        return self._wrap(fd, d, n)
+
+    def imag_steps(self, m: MPS, U, tau, nsteps) -> MPS:
+        """nsteps imaginary-time steps exp(-tau H(J, U)) (ground-state preparation)"""
+        fd, d, n = self._out()
+        _, pd = _i(m.dims)
+        raw, pr = _d(m.raw())
+        self._chk(lib().ocg_imag_steps(self.h, pd, pr, float(U), float(tau), int(nsteps), fd.ctypes.data_as(ip),
+                                       d.ctypes.data_as(dp), self.cap, C.byref(n)), "ocg_imag_steps")
         return self._wrap(fd, d, n)
 
     def step_batch(self, states, u_from, u_to, forward=True):

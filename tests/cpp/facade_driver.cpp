@@ -28,6 +28,7 @@
 using Stepper = ocmps_test::OracleTDMRG;
 #else
 #include "../../optimalcontrolmps_amd/include/optimalcontrolmps/GpuTDMRG.hpp"
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/InitializeState.hpp"
 using Stepper = ocmps::GpuTDMRG;
 #endif
 
@@ -548,6 +549,21 @@ static void scen_config3(Json& js, const std::vector<int>& shard_counts) {
   js.vec("group_grad", group.getAnalyticGradient(c));
 }
 
+#ifndef OCMPS_ORACLE
+// InitializeState (include/InitializeState.hpp:18-117) on the device, as the
+// drivers call it (main/OptimizeRamp.cpp:84-85): the states as flat arrays
+static void scen_initstate(Json& js) {
+  BoseHubbard sites(5, 4);
+  for (double U : {2.5, 50.0}) {
+    const MPS psi = ocmps::InitializeState(sites, 5, 1.0, U, 80, 1e-9);
+    const std::string k = U < 10 ? "U2.5" : "U50";
+    stdvec d(psi.dims.begin(), psi.dims.end()), x(psi.raw(), psi.raw() + 2 * psi.data.size());
+    js.vec(k + "_dims", d);
+    js.vec(k + "_data", x);
+  }
+}
+#endif
+
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s <basis|cost|gradient|hessian|sequencing|golden|nlp> <state-dir>\n", argv[0]);
@@ -564,6 +580,9 @@ int main(int argc, char** argv) {
     else if (sc == "sequencing") scen_sequencing(js);
     else if (sc == "golden") scen_golden(js);
     else if (sc == "nlp") scen_nlp(js);
+#ifndef OCMPS_ORACLE
+    else if (sc == "initstate") scen_initstate(js);
+#endif
     else if (sc == "config3") {
       std::vector<int> gs;
       if (argc > 3) {
