@@ -22,6 +22,7 @@
 #include "../../optimalcontrolmps_amd/include/optimalcontrolmps/ControlBasisFactory.hpp"
 #include "../../optimalcontrolmps_amd/include/optimalcontrolmps/OptimalControl.hpp"
 #include "../../optimalcontrolmps_amd/include/optimalcontrolmps/SeedGenerator.hpp"
+#include "../../optimalcontrolmps_amd/include/optimalcontrolmps/correlations.hpp"
 
 #ifdef OCMPS_ORACLE
 #include "oracle_stepper.hpp"
@@ -549,6 +550,73 @@ static void scen_config3(Json& js, const std::vector<int>& shard_counts) {
   js.vec("group_grad", group.getAnalyticGradient(c));
 }
 
+// correlations.hpp (the drivers' observables) on a ground state and on a
+// time-evolved state (complex, centre moved by the stepper); the states are
+// returned too, so the test recomputes every value from the full state vector
+static void scen_observables(Json& js) {
+  BoseHubbard sites(5, 4);
+  MPS gs = load_state(skey(5, 5, 5, 1.0, 2.5));
+  Stepper st(sites, 1.0, 0.01, Args(1e-10, 80));
+  MPS ev = gs;
+  for (int k = 0; k < 5; ++k) st.step(ev, 2.5 + 3 * k, 5.5 + 3 * k, true);
+  const std::pair<const char*, const MPS*> cases[] = {{"gs", &gs}, {"ev", &ev}};
+  for (auto& [tag, m] : cases) {
+    const std::string t(tag);
+    stdvec d(m->dims.begin(), m->dims.end()), x(m->raw(), m->raw() + 2 * m->data.size());
+    js.vec(t + "_dims", d);
+    js.vec(t + "_data", x);
+    for (const char* op : {"N", "NN", "N(N-1)", "Id", "A"}) {
+      const auto e = ocmps::expectationValues(sites, *m, op);
+      stdvec re, im;
+      for (auto& v : e) { re.push_back(v.real()); im.push_back(v.imag()); }
+      js.vec(t + "_exp_" + op + "_re", re);
+      js.vec(t + "_exp_" + op + "_im", im);
+    }
+    for (auto pr : {std::make_pair("Adag", "A"), std::make_pair("N", "N")}) {
+      const auto rho = ocmps::correlationMatrix(sites, *m, pr.first, pr.second);
+      rowmat re(rho.size()), im(rho.size());
+      for (size_t i = 0; i < rho.size(); ++i)
+        for (auto& v : rho[i]) { re[i].push_back(v.real()); im[i].push_back(v.imag()); }
+      js.mat(t + "_corr_" + pr.first + pr.second + "_re", re);
+      js.mat(t + "_corr_" + pr.first + pr.second + "_im", im);
+    }
+    const Cplx c41 = ocmps::correlationFunction(sites, *m, "Adag", 4, "A", 1);
+    js.num(t + "_c41_re", c41.real());
+    js.num(t + "_c41_im", c41.imag());
+    js.num(t + "_term", ocmps::correlationTerm(sites, *m, "Adag", "A"));
+    js.vec(t + "_entropy", ocmps::entanglementEntropy(sites, *m));
+  }
+}
+
+// main/ExtendTimeEvolution.cpp's computation (without its file I/O): two
+// ramps extended by 100 constant steps, fidelities for all t
+// (getFidelityForAllT) and <N_i>(t) along psi_t (getPsit + expectationValues)
+static void scen_extend(Json& js) {
+  BoseHubbard sites(5, 4);
+  const double tstep = 0.01;
+  const int Nt = 101;
+  stdvec u_init = SeedGenerator::linspace(2.5, 50.0, Nt), u_final = SeedGenerator::linsigmoidSeed(2.5, 50.0, Nt);
+  for (int i = 1; i <= 100; ++i) {
+    u_init.push_back(u_init.back());
+    u_final.push_back(u_final.back());
+  }
+  MPS psi_i = load_state(skey(5, 5, 5, 1.0, 2.5)), psi_f = load_state(skey(5, 5, 5, 1.0, 50.0));
+  Stepper stepper(sites, 1.0, tstep, Args(1e-12, 200));  // truncation below the exact-evolution check
+  OC oc(psi_f, psi_i, stepper, u_init.size(), 0.0);
+  js.vec("u_init", u_init);
+  js.vec("u_final", u_final);
+  js.vec("fid_init", oc.getFidelityForAllT(u_init));
+  js.vec("fid_final", oc.getFidelityForAllT(u_final));
+  const auto psi_t = oc.getPsit();
+  rowmat expN;
+  for (const auto& psi : psi_t) {
+    stdvec row;
+    for (auto& v : ocmps::expectationValues(sites, psi, "N")) row.push_back(v.real());
+    expN.push_back(row);
+  }
+  js.mat("expN_final", expN);
+}
+
 #ifndef OCMPS_ORACLE
 // InitializeState (include/InitializeState.hpp:18-117) on the device, as the
 // drivers call it (main/OptimizeRamp.cpp:84-85): the states as flat arrays
@@ -583,6 +651,8 @@ int main(int argc, char** argv) {
 #ifndef OCMPS_ORACLE
     else if (sc == "initstate") scen_initstate(js);
 #endif
+    else if (sc == "observables") scen_observables(js);
+    else if (sc == "extend") scen_extend(js);
     else if (sc == "config3") {
       std::vector<int> gs;
       if (argc > 3) {
