@@ -60,11 +60,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak")
-    ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c4rows"], default="hessian")
+    ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c4rows", "c5rows"], default="hessian")
     ap.add_argument("--c4-nt", type=int, default=33)
+    ap.add_argument("--c5-nt", type=int, default=5)
+    ap.add_argument("--c5-warm", type=int, default=230)
     ap.add_argument("--profile-tag", default="r02")
     args = ap.parse_args()
-    if args.workload in ("c4grad", "c4rows"):
+    if args.workload in ("c4grad", "c4rows", "c5rows"):
         return bench_c4(args)
 
     rank = int(os.environ.get("RANK", "0"))
@@ -271,6 +273,7 @@ def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, dev):
 
 
 C4 = dict(L=20, p=7, npart=20, J=1.0, tstep=0.005, T=4.0, maxm=256, cutoff=1e-8, seed=20261016)
+C5 = dict(L=50, p=9, npart=50, J=1.0, tstep=0.01, T=10.0, maxm=512, cutoff=1e-8, seed=20261017)
 
 
 def bench_c4(args):
@@ -280,18 +283,32 @@ def bench_c4(args):
     psi_target = psi_init evolved 2 more steps at U=6 (config 4's |1..1> target has
     ~1e-10 overlap, which leaves every derivative at rounding level; cost is
     independent of the target).  GRAPE controls U(2,10); the GROUP M=40 projection
-    is a host GEMM (ControlBasis) and not part of the timed device work."""
+    is a host GEMM (ControlBasis) and not part of the timed device work.
+
+    c5rows: config 5's chain (BASELINE configs[4]: L=50 Npart=50 d=8 chi=512
+    tstep=0.01): psi_init = the Mott state |1..1> evolved --c5-warm steps at U=2.5
+    on the device (untimed; the bonds saturate at 512 after ~220 steps), a
+    getHessian slice of --c5-nt time points (the aspirational scaling slice of
+    SURVEY.md §8d)."""
     import torch
     from optimalcontrolmps_amd.native import MPS, Engine
-    c = C4
+    c5 = args.workload == "c5rows"
+    c = C5 if c5 else C4
     L, p, Q, dt = c["L"], c["p"], c["npart"], c["tstep"]
-    z = np.load(os.path.join(ROOT, "tests", "golden", "c4_warm256.npz"), allow_pickle=False)
-    ini = MPS(L, p, Q, z["dims"], z["data"])
     eng = Engine(L, p, Q, c["J"], dt, c["cutoff"], c["maxm"], device=0, engine="hbm")
+    if c5:
+        from optimalcontrolmps_amd.states import product_state, warm_state
+        t0 = time.perf_counter()
+        ini = warm_state(eng, product_state(L, p, Q), 2.5, args.c5_warm, chunk=10)
+        warm_s = time.perf_counter() - t0
+    else:
+        z = np.load(os.path.join(ROOT, "tests", "golden", "c4_warm256.npz"), allow_pickle=False)
+        ini = MPS(L, p, Q, z["dims"], z["data"])
+        warm_s = 0.0
     tgt = eng.steps(ini, np.full(3, 6.0), True)
     eng.set_states(tgt, ini)
     grad = args.workload == "c4grad"
-    Nt = int(round(c["T"] / dt)) + 1 if grad else args.c4_nt
+    Nt = int(round(c["T"] / dt)) + 1 if grad else (args.c5_nt if c5 else args.c4_nt)
     u = np.random.default_rng(c["seed"]).uniform(2.0, 10.0, Nt)
     rows = list(range(1, Nt - 1))
 
@@ -324,14 +341,18 @@ def bench_c4(args):
     gemm_ms = gm["ms"] / max(1, gm["launches"])
     res = {
         "metric": ("getAnalyticGradient/sec (psi || xi + divT)" if grad else "Hessian-rows/sec (getHessian fidelity part)")
-                  + ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005",
+                  + (", config 5 chain L=50 Npart=50 d=8 chi=512 tstep=0.01" if c5 else
+                     ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005"),
         "value": (args.steps if grad else args.steps * (Nt - 2)) / elapsed,
         "unit": "gradients/s" if grad else "rows/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c128/f64",
-        "data": "synthetic GRAPE controls U(2,10) seed 20261016; psi_init = saturated chi=256 warm state",
+        "data": (f"synthetic GRAPE controls U(2,10) seed {c['seed']}; psi_init = "
+                 + (f"|1..1> evolved {args.c5_warm} steps at U=2.5 on the device (untimed, {warm_s:.0f} s; "
+                    f"max bond {int(ini.bond_dims().max())})" if c5 else "saturated chi=256 warm state")),
         "config": {"workload": (f"config 4 chain, getAnalyticGradient over N_t={Nt} (T=4)" if grad else
-                                f"config 4 chain, getHessian over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)"),
+                                f"config {5 if c5 else 4} chain, getHessian over a T slice N_t={Nt} "
+                                f"({Nt - 2} rows, {row_steps} row-steps)"),
                    "engine": "HBM-resident (hbm.hip)"},
         "sweep_steps_per_sec": sweep / elapsed,
         "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(st_traj["ms"] / max(1, st_traj["launches"]), 1e-9),
@@ -340,7 +361,7 @@ def bench_c4(args):
                       "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,
                       "achieved_gbs": gm["alg_bytes"] / max(gm["ms"], 1e-9) / 1e6},
         "roofline": roofline_block("hbm::k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
-                                   gm["alg_flops"] / max(1, gm["launches"]), args.profile_tag + "c4",
+                                   gm["alg_flops"] / max(1, gm["launches"]), args.profile_tag + ("c5" if c5 else "c4"),
                                    limiter="the per-sector Hermitian eigensolver (k_heev_*: one CU per block, "
                                            "latency-bound), not the MFMA contraction"),
     }

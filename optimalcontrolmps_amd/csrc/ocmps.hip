@@ -547,8 +547,11 @@ int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, d
     ocg_destroy(c);
     return code;
   };
-  if (L < 2 || L > OCG_MAXL || p < 2 || p > OCG_MAXP || npart < 0 || npart + 1 > OCG_MAXQ1 ||
-      npart > L * (p - 1) || !(tstep == tstep) || !(cutoff >= 0)) {
+  // the LDS chain engine's parameter block holds up to OCG_MAXL sites and
+  // OCG_MAXQ1 sectors; the HBM engine takes up to 63 sites (config 5: L = 50)
+  const bool lds_fits = L <= OCG_MAXL && npart + 1 <= OCG_MAXQ1;
+  if (L < 2 || L > 63 || p < 2 || p > OCG_MAXP || npart < 0 || npart + 1 > 1024 || npart > L * (p - 1) ||
+      !(tstep == tstep) || !(cutoff >= 0) || (engine == 1 && !lds_fits)) {
     int rc = build_params(c, L, p, npart, tstep, cutoff, maxm);  // same messages as before
     if (!rc) { c->err = "bad argument"; rc = OCG_EINVAL; }
     return bail(rc);
@@ -563,7 +566,7 @@ int ocg_create_ex(int device, int L, int p, int npart, double J, double tstep, d
   if (hipSetDevice(device) != hipSuccess) { c->err = "hipSetDevice failed"; return bail(OCG_EHIP); }
   if (!make_stream(c)) return bail(OCG_EHIP);
   int rc = 0;
-  if (engine != 2) {
+  if (engine != 2 && lds_fits) {
     rc = build_params(c, L, p, npart, tstep, cutoff, maxm);
     // gate tables first: their size (gtotal) is part of the LDS layout
     if (!rc) rc = upload_gates(c);
