@@ -929,21 +929,24 @@ struct Engine {
     copy(ct);
   }
   // |site k|^2 of every view (one reduction launch, host readback)
+  // (k_sumsq: one workgroup per view, fixed summation order: deterministic)
   std::vector<double> site_norm2(const std::vector<View>& vs, int k) {
+    if (vs.empty()) return {};
     double* acc = walloc<double>(vs.size());
-    HCK(hipMemsetAsync(acc, 0, sizeof(double) * vs.size(), st));
     std::vector<CTask> ct;
+    std::vector<int> t0(vs.size() + 1, 0);
     for (size_t i = 0; i < vs.size(); ++i) {
       const Dims& d = *vs[i].d;
       SiteLayout sl = site_layout(d, k, p);
       for (int q = 0; q < Q1; ++q) {
-        if (sl.lmat[q] < 0) continue;
-        CTask c = ctask(vs[i].site[k] + sl.lmat[q], nullptr, sl.lrows[q], d(k, q), d(k, q), 0, 4);
-        c.acc = acc + i;
-        ct.push_back(c);
+        if (sl.lmat[q] < 0 || sl.lrows[q] <= 0 || d(k, q) <= 0) continue;
+        ct.push_back(ctask(vs[i].site[k] + sl.lmat[q], nullptr, sl.lrows[q], d(k, q), d(k, q), 0, 4));
       }
+      t0[i + 1] = int(ct.size());
     }
-    copy(ct);
+    if (ct.empty()) ct.push_back(ctask(nullptr, nullptr, 0, 0, 0, 0, 4));  // every view empty: sums of nothing
+    hipLaunchKernelGGL(k_sumsq, dim3(unsigned(vs.size())), dim3(NT), 0, st, upload(ct), upload(t0), acc);
+    HCK(hipGetLastError());
     std::vector<double> h(vs.size());
     HCK(hipMemcpyAsync(h.data(), acc, sizeof(double) * vs.size(), hipMemcpyDeviceToHost, st));
     sync();
@@ -1871,6 +1874,175 @@ int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int
       for (auto* c : cs) E.release(c);
     }
     t.stop(nsteps);
+  });
+}
+
+double hbm_traj_bytes(const hbm_engine* h, int N) { return 16.0 * double(h->E->state_cap) * (3.0 * N + 6.0); }
+
+// Checkpointed getHessian (see hbm.hpp).  Time-major row sweep: all rows of a
+// batch advance together in absolute time j (row i joins at j = i with
+// psiH_i = dH psi_i), so every active row needs the same xiH_j at step j and
+// psi_i only when it joins; both are produced segment by segment from the
+// checkpoints (psi forward from psi_{T_s}, xi backward from xi_{T_{s+1}}).
+// Same steps, decompositions, dH applications and overlaps as the stored
+// path, so the same numbers bit for bit (every kernel is batch-independent
+// and deterministic).
+int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                     double* F, int K) {
+  return guard(h, [&] {
+    if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
+    if (N < 2) throw hbm::Error(1, "N < 2");
+    hbm::Engine& E = *h->E;
+    K = std::max(1, std::min(K, N - 1));
+    const int S = (N - 1 + K - 1) / K;  // segments s = 0..S-1 cover [T_s, T_{s+1}], T_S = N - 1
+    auto Tc = [&](int s) { return std::min(s * K, N - 1); };
+    // slots: 0 init, 1 target, then ckpsi[S+1], ckxi[S+1], segpsi[K+1], segxi[K+1], segxiH[K+1]
+    const int ckp = 2, ckx = ckp + S + 1, sgp = ckx + S + 1, sgx = sgp + K + 1, sgh = sgx + K + 1;
+    E.reserve_states(size_t(sgh + K + 1));
+    h->have_psi = h->have_xi = h->have_xih = false;  // the trajectory slots are overwritten
+    h->N = 0;
+    const double dt2 = E.dt * E.dt;
+    Timer tall(h, 5);
+    // 1. psi forward / xi backward in one batch, checkpoints only
+    E.reserve_chains(std::max(E.nchain_cap, 2), false);
+    {
+      std::vector<Chain*> cs{E.acquire(false), E.acquire(false)};
+      E.load_many(cs, {E.states[0].view(), E.states[1].view()});
+      E.store_many({&E.states[ckp], &E.states[ckx + S]}, cs);
+      std::vector<double> uf(2), ut(2);
+      std::vector<int> fw{1, 0};
+      for (int s = 0; s + 1 < N; ++s) {
+        uf[0] = u[s]; ut[0] = u[s + 1];
+        uf[1] = u[N - 1 - s]; ut[1] = u[N - 2 - s];
+        E.step(cs, uf, ut, fw);
+        const int tp = s + 1, tx = N - 2 - s;
+        std::vector<State*> ss;
+        std::vector<Chain*> cc;
+        if (tp == N - 1 || tp % K == 0) { ss.push_back(&E.states[ckp + (tp == N - 1 ? S : tp / K)]); cc.push_back(cs[0]); }
+        if (tx % K == 0) { ss.push_back(&E.states[ckx + tx / K]); cc.push_back(cs[1]); }
+        if (!ss.empty()) E.store_many(ss, cc);
+      }
+      E.sync();
+      for (auto* c : cs) E.release(c);
+    }
+    // F = overlapC(psi_{N-1}, target) (:242)
+    const std::complex<double> Fc = E.overlaps({E.states[ckp + S].view()}, {E.states[1].view()}, false)[0];
+    F[0] = Fc.real();
+    F[1] = Fc.imag();
+    std::vector<std::complex<double>> dv(N, 0.0);
+    // 2. row batches (ascending rows; the first pass also forms divT everywhere)
+    std::vector<int> rs(rows, rows + nrows);
+    std::sort(rs.begin(), rs.end());
+    const int B = std::max(1, hbm_batch(h, std::max(nrows, 1)));
+    E.reserve_chains(std::max(E.nchain_cap, std::max(B, 2)), false);
+    bool first = true;
+    for (int r0 = 0; first || r0 < nrows; r0 += B) {
+      const int nb = std::min(B, nrows - r0);
+      const int imin = nb > 0 ? rs[r0] : N;
+      std::vector<Chain*> act;  // active rows, in joining order
+      std::vector<int> ai;      // their i
+      std::vector<double> nrm;
+      int next = r0;            // next row of the batch to join
+      const int s_begin = first ? 0 : std::min(S - 1, imin / K);
+      for (int s = s_begin; s < S; ++s) {
+        const int a = Tc(s), b = Tc(s + 1);  // segment [a, b]
+        const bool need_rows = nb > 0 && b - 1 >= imin && a <= N - 2;
+        if (!first && !need_rows) continue;
+        // psi_a..psi_b forward from the checkpoint
+        {
+          std::vector<Chain*> c1{E.acquire(false)};
+          E.load_many(c1, {E.states[ckp + s].view()});
+          E.store_many({&E.states[sgp]}, c1);
+          for (int t = a; t < b; ++t) {
+            E.step(c1, {u[t]}, {u[t + 1]}, {1});
+            E.store_many({&E.states[sgp + t + 1 - a]}, c1);
+          }
+          E.sync();
+          E.release(c1[0]);
+        }
+        // xi_b..xi_a backward from the checkpoint
+        {
+          std::vector<Chain*> c1{E.acquire(false)};
+          E.load_many(c1, {E.states[ckx + s + 1].view()});
+          E.store_many({&E.states[sgx + b - a]}, c1);
+          for (int t = b; t > a; --t) {
+            E.step(c1, {u[t]}, {u[t - 1]}, {0});
+            E.store_many({&E.states[sgx + t - 1 - a]}, c1);
+          }
+          E.sync();
+          E.release(c1[0]);
+        }
+        // divT_t = overlapC(xi_t, dH, psi_t) (:409-419), t in [a, b) (and N-1 at the end)
+        if (first) {
+          std::vector<View> xs, ys;
+          const int tend = (s == S - 1) ? b : b - 1;
+          for (int t = a; t <= tend; ++t) { xs.push_back(E.states[sgx + t - a].view()); ys.push_back(E.states[sgp + t - a].view()); }
+          const auto r = E.overlaps(xs, ys, true);
+          for (int t = a; t <= tend; ++t) dv[t] = r[t - a];
+        }
+        if (!need_rows) continue;
+        // xiH_j = exactApplyMPO(dH, xi_j) for the rows' times in this segment (:300-303)
+        const int j0 = std::max(a, imin), j1 = std::min(b - 1, N - 2);
+        {
+          std::vector<View> in;
+          std::vector<Chain*> out;
+          std::vector<State*> ss;
+          for (int j = j0; j <= j1; ++j) {
+            in.push_back(E.states[sgx + j - a].view());
+            out.push_back(E.acquire(false));
+            ss.push_back(&E.states[sgh + j - a]);
+          }
+          E.apply_dH(in, out);
+          E.store_many(ss, out);
+          E.sync();
+          for (auto* c : out) E.release(c);
+        }
+        for (int j = j0; j <= j1; ++j) {
+          // active rows: step u[j-1] -> u[j] (timeStepper.step(psiH, ..), :269), overlap with xiH_j
+          if (!act.empty()) {
+            E.step(act, std::vector<double>(act.size(), u[j - 1]), std::vector<double>(act.size(), u[j]),
+                   std::vector<int>(act.size(), 1));
+            std::vector<View> xs(act.size(), E.states[sgh + j - a].view()), ys;
+            for (auto* c : act) ys.push_back(c->view());
+            const auto ov = E.overlaps(xs, ys, false);
+            for (size_t m = 0; m < act.size(); ++m) {
+              const int i = ai[m];
+              const double v1 = (Fc * ov[m] * nrm[m]).real();
+              const double v2 = -(dv[i] * std::conj(dv[j])).real();
+              const double r = dt2 * (v1 + v2);
+              H[size_t(i) * N + j] = r;
+              H[size_t(j) * N + i] = r;
+            }
+          }
+          // rows joining at j: psiH_i = dH psi_i, normiH, diagonal (:256-264)
+          std::vector<int> join;
+          while (next < r0 + nb && rs[next] == j) join.push_back(rs[next++]);
+          if (!join.empty()) {
+            std::vector<View> in(join.size(), E.states[sgp + j - a].view());
+            std::vector<Chain*> cs;
+            for (size_t m = 0; m < join.size(); ++m) cs.push_back(E.acquire(false));
+            E.apply_dH(in, cs);
+            std::vector<View> vs;
+            for (auto* c : cs) vs.push_back(c->view());
+            const std::vector<double> n2 = E.site_norm2(vs, 1);
+            std::vector<View> xs(join.size(), E.states[sgh + j - a].view());
+            const auto ov = E.overlaps(xs, vs, false);
+            for (size_t m = 0; m < join.size(); ++m) {
+              const int i = join[m];
+              H[size_t(i) * N + i] = dt2 * ((Fc * ov[m]).real() - std::norm(dv[i]));
+              act.push_back(cs[m]);
+              ai.push_back(i);
+              nrm.push_back(std::sqrt(std::max(0.0, n2[m])));
+            }
+          }
+        }
+      }
+      for (auto* c : act) E.release(c);
+      first = false;
+      if (nb <= 0) break;
+    }
+    for (int t = 0; t < N; ++t) { divT[2 * t] = dv[t].real(); divT[2 * t + 1] = dv[t].imag(); }
+    tall.stop();
   });
 }
 

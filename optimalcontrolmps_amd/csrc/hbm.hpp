@@ -40,6 +40,15 @@ int hbm_div_t(hbm_engine* h, double* divT);
 int hbm_xi_dH(hbm_engine* h);
 int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int nrows, const double* F,
                      const double* divT, double* H);
+// getHessian's fidelity part (psi, xi, divT, F, rows) with trajectory
+// checkpointing: psi_t / xi_t kept only every K steps,
+// segments recomputed, xiHlist formed one segment at a time; O(N/K + K + rows
+// of a batch) states instead of 3 N.  Bit-identical to the stored path.
+// Leaves no device trajectories (ocg_get_state fails afterwards).
+int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                     double* F, int K);
+// states the stored-trajectory Hessian would keep (3 N + 6) x bytes per state
+double hbm_traj_bytes(const hbm_engine* h, int N);
 int hbm_get_state(hbm_engine* h, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
 // kinds 0-6 as ocg_kernel_stats (HIP-event phase times); 7: the MFMA GEMM
 // kernel (k_gemm) with its algorithmic bytes and flops

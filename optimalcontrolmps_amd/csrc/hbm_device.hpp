@@ -70,8 +70,8 @@ struct GTask {
   int tile0;  // prefix of 32x32 tiles over tasks
 };
 // element copies: dst[i][j] = f * rs[i] * cs[j] * sc * (conj^T? conj(src[j][i]) : src[i][j])
-// mode bit 0: conj-transpose, bit 1: zero fill (src unused), bit 2: |.|^2
-// accumulate into *acc (reduction task, dst unused), bit 3: fill with f.
+// mode bit 0: conj-transpose, bit 1: zero fill (src unused), bit 2: sum of
+// squares (k_sumsq's task lists only), bit 3: fill with f.
 struct CTask {
   const z* src;
   z* dst;
@@ -81,7 +81,6 @@ struct CTask {
   const double* rs;
   const double* cs;
   const double* sc;
-  double* acc;
   long long e0;  // prefix of elements over tasks
 };
 
@@ -195,11 +194,6 @@ __global__ __launch_bounds__(NT) void k_copy(const CTask* __restrict__ tasks, in
     const CTask& T = tasks[ti];
     const long long x = e - T.e0;
     const int i = int(x / T.cols), j = int(x - (long long)i * T.cols);
-    if (T.mode & 4) {  // |src[i][j]|^2 into *acc
-      const z v = T.src[(size_t)i * T.lds + j];
-      atomicAdd(T.acc, v.x * v.x + v.y * v.y);
-      continue;
-    }
     z v = (T.mode & 8) ? T.f : mk(0, 0);
     if (!(T.mode & 10)) {
       v = (T.mode & 1) ? zcj(T.src[(size_t)j * T.lds + i]) : T.src[(size_t)i * T.lds + j];
@@ -306,6 +300,29 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
 #pragma unroll
   for (int i = 0; i < NT / 64; ++i) s += red[i];
   return s;
+}
+
+// sum |x|^2 over the tasks [t0[b], t0[b+1]) of view b, one workgroup per view:
+// every thread sums a fixed set of elements, then a fixed-order tree, so the
+// result does not depend on scheduling or on the other views of the launch
+// (an atomicAdd per element made the norms, and with them every normalised
+// state, vary in the last bits from run to run)
+__global__ __launch_bounds__(NT) void k_sumsq(const CTask* __restrict__ tasks, const int* __restrict__ t0,
+                                              double* __restrict__ out) {
+  __shared__ double red[NT / 64];
+  const int b = blockIdx.x;
+  double s = 0;
+  for (int t = t0[b]; t < t0[b + 1]; ++t) {
+    const CTask& T = tasks[t];
+    const long long n = (long long)T.rows * T.cols;
+    for (long long x = threadIdx.x; x < n; x += NT) {
+      const int i = int(x / T.cols), j = int(x - (long long)i * T.cols);
+      const z v = T.src[(size_t)i * T.lds + j];
+      s += v.x * v.x + v.y * v.y;
+    }
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[b] = s;
 }
 
 constexpr int kLdsOrder = 88;  // Gram blocks up to this order are reduced inside LDS

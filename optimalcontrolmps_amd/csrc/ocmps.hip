@@ -1058,6 +1058,22 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   if (c->hbm) {
     for (int r = 0; r < nrows; ++r)
       if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
+    // trajectory checkpointing when psi_t + xi_t + xiH_t would not fit half of
+    // the free HBM (config 5: ~600 GB at N_t = 1001), or when OCG_HBM_CKPT=K asks
+    // for it (segment length K; tests, A/B)
+    int K = 0;
+    if (const char* e = std::getenv("OCG_HBM_CKPT")) K = std::atoi(e);
+    if (K <= 0) {
+      size_t fr = 0, tot = 0;
+      HIPCHK(c, hipSetDevice(c->device));
+      HIPCHK(c, hipMemGetInfo(&fr, &tot));
+      if (hbm_traj_bytes(c->hbm, N) > 0.5 * double(fr)) K = std::max(1, int(std::ceil(std::sqrt(double(N)))));
+    }
+    if (K > 0) {
+      c->u_psi.clear();
+      c->u_xi.clear();
+      return hb(c, hbm_hessian_ckpt(c->hbm, u, N, rows, nrows, H, divT, F, K));
+    }
     return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
   }
   if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");

@@ -1,0 +1,74 @@
+"""Trajectory checkpointing of the HBM engine: the
+Hessian with psi_t / xi_t kept every K steps, segments recomputed and
+xiHlist formed segment by segment (hbm_hessian_ckpt, selected automatically
+when psi_t + xi_t + xiH_t would not fit half the free HBM — config 5 at full
+N_t — or by OCG_HBM_CKPT=K) must equal the stored-trajectory path bit for bit:
+the same steps, decompositions and overlaps run in another order, and every
+HBM-engine kernel is batch-independent and deterministic."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import state_key
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = pytest.mark.gpu
+
+
+def stored(eng, u, rows):
+    eng.propagate(u, 3)
+    divT = eng.div_t()
+    F = eng.overlap_factor()
+    eng.xi_dH()
+    return eng.hessian_rows(u, rows, F, divT), divT, F
+
+
+def ckpt(eng, u, rows, K):
+    os.environ["OCG_HBM_CKPT"] = str(K)
+    try:
+        return eng.hessian(u, rows)
+    finally:
+        del os.environ["OCG_HBM_CKPT"]
+
+
+@pytest.mark.parametrize("K", [1, 3, 8])
+def test_ckpt_config1_states_bitwise(states, K):
+    from optimalcontrolmps_amd.native import MPS, Engine
+    L, p, N, J = 5, 5, 5, 1.0
+
+    def st(U):
+        k = state_key(L, p, N, J, U)
+        return MPS(L, p, N, states[k + "/dims"], states[k + "/data"])
+    u = np.random.default_rng(31).uniform(2, 10, 21)
+    rows = list(range(1, 20))
+    eng = Engine(L, p, N, J, 0.01, 1e-8, 80, engine="hbm")
+    eng.set_states(st(50.0), st(2.5))
+    H1, d1, F1 = stored(eng, u, rows)
+    H2, d2, F2 = ckpt(eng, u, rows, K)
+    assert F1 == F2 and np.array_equal(d1, d2)
+    assert np.array_equal(H1, H2)
+    # a row subset in two batches of the time-major sweep
+    sub = [3, 4, 11, 17]
+    H3, _, _ = ckpt(eng, u, sub, K)
+    for i in sub:
+        assert np.array_equal(H3[i, i:19], H1[i, i:19]) and np.array_equal(H3[i:19, i], H1[i:19, i])
+
+
+def test_ckpt_config4_s32_vs_oracle():
+    """config 4's chain (L=20 p=7, Maxm 32): checkpointed Hessian vs the oracle
+    fixture at the north_star tolerances and bitwise vs the stored path"""
+    from optimalcontrolmps_amd.native import MPS, Engine
+    L, p, N, J, DT, CUT = 20, 7, 20, 1.0, 0.005, 1e-8
+    c4 = dict(np.load(os.path.join(HERE, "golden", "c4.npz"), allow_pickle=False))
+    u = c4["s32/u"]
+    Nt = len(u)
+    eng = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+    eng.set_states(MPS(L, p, N, c4["s32/tgt_dims"], c4["s32/tgt_data"]),
+                   MPS(L, p, N, c4["s32/init_dims"], c4["s32/init_data"]))
+    rows = list(range(1, Nt - 1))
+    H1, d1, F1 = stored(eng, u, rows)
+    H2, d2, F2 = ckpt(eng, u, rows, 3)
+    assert np.array_equal(H1, H2) and np.array_equal(d1, d2) and F1 == F2
+    Ho = c4["s32/H"]
+    assert np.abs(H2 - Ho).max() <= 1e-6 * np.abs(Ho).max()
