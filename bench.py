@@ -75,11 +75,17 @@ def main():
 
     import torch
     dist = None
+    # OCG_BENCH_BACKEND=gloo (dry runs of the multi-rank path with several ranks
+    # per GPU): ranks map onto the visible devices round-robin, collectives on
+    # host tensors.  Default: nccl (= RCCL over xGMI), one rank per GPU.
+    backend = os.environ.get("OCG_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")
 
     from optimalcontrolmps_amd import ed
     from optimalcontrolmps_amd.native import MPS, Engine
@@ -96,10 +102,10 @@ def main():
 
     eng = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
     eng.set_states(tgt, ini)
-    Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=dev)
+    Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=cdev)
 
     if args.workload == "gradient":
-        return bench_gradient(args, eng, u, Nt, dt, world, rank, dist, dev)
+        return bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev)
 
     def one_step():
         # fused getHessian: psi/xi chains, xiHlist and this rank's rows in one
@@ -127,7 +133,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -219,7 +225,7 @@ def roofline_block(kernel, launch_ms, bytes_per_launch, flops_per_launch, tag, l
     }
 
 
-def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, dev):
+def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev):
     """config 2: getAnalyticGradient(u) with BFGS=true at config 1 — psi_t and xi_t
     propagated concurrently in one launch (calcFidelityGrad's BFGS branch,
     src/OptimalControl.cpp:217-229, propagates xi independently of psi), then the
@@ -246,7 +252,7 @@ def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     st_traj, st_ov = eng.stats(0), eng.stats(1)
