@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--c4-nt", type=int, default=33)
     ap.add_argument("--c5-nt", type=int, default=5)
     ap.add_argument("--c5-warm", type=int, default=230)
+    ap.add_argument("--controls", type=int, default=1,
+                    help="K control vectors per GPU evaluated concurrently (K contexts, one host thread and "
+                         "stream each: IPOPT trial points / multi-start); value = rows of all K per second")
     ap.add_argument("--profile-tag", default="r02")
     args = ap.parse_args()
     if args.workload in ("c4grad", "c4rows", "c5rows"):
@@ -102,16 +105,30 @@ def main():
 
     eng = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
     eng.set_states(tgt, ini)
+    K = max(1, args.controls)
+    extra = []  # controls 2..K of this GPU: own context + stream, own control vector
+    for k in range(1, K):
+        e2 = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
+        e2.set_states(tgt, ini)
+        extra.append((e2, np.random.default_rng(CFG["seed"] + 1000 * k + rank).uniform(2.0, 10.0, Nt)))
     Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=cdev)
 
     if args.workload == "gradient":
         return bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev)
 
+    pool = None
+    if extra:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(len(extra))   # ctypes releases the GIL inside ocg_hessian
+
     def one_step():
         # fused getHessian: psi/xi chains, xiHlist and this rank's rows in one
         # pipelined launch (rows start as their psi_i appears), then divT, F
         # and the batched <xiH_j|psiH> overlaps (ocg_hessian)
+        futs = [pool.submit(e2.hessian, u2, rows) for e2, u2 in extra] if extra else []
         H, divT, F = eng.hessian(u, rows)
+        for f in futs:
+            f.result()
         g = dt * (divT * F * 1j).real            # calcFidelityGrad (gamma = 0)
         if world > 1 and strong:
             Hdev.copy_(torch.from_numpy(H))
@@ -137,7 +154,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    rows_total = (Nt - 2) * args.steps * (1 if strong else world)
+    rows_total = (Nt - 2) * args.steps * (1 if strong else world) * K
     value = rows_total / elapsed
     st_rows = eng.stats(5)       # k_pipeline: trajectories + row re-propagation (dominant)
     st_ovl = eng.stats(6)        # k_row_overlaps
@@ -145,7 +162,7 @@ def main():
     eng.propagate(u, 3)          # one bare psi || xi trajectory (outside the timed region): single-chain step rate
     t_tr = time.perf_counter() - t_tr
     row_steps = (Nt - 2) * (Nt - 3) // 2
-    sweep_steps = args.steps * (2 * (Nt - 1) * world + row_steps * (1 if strong else world))
+    sweep_steps = args.steps * K * (2 * (Nt - 1) * world + row_steps * (1 if strong else world))
     result = None
     if rank == 0:
         launch_ms = st_rows["ms"] / max(1, st_rows["launches"])
@@ -166,8 +183,9 @@ def main():
             "dtype": "c128/f64",
             "data": "synthetic GRAPE controls U(2,10) seed 20261015; ED ground states U=2.5 -> 50",
             "config": {"workload": "getHessian(u, new_control=true), config 1 (L=5 Npart=5 d=4 maxBondDim=80 "
-                                   "tstep=0.01 T=2.0 GRAPE, N_t=201, 199 rows)",
-                       "rows_per_step": (Nt - 2) * (1 if strong else world),
+                                   "tstep=0.01 T=2.0 GRAPE, N_t=201, 199 rows)"
+                                   + (f", {K} concurrent control vectors per GPU" if K > 1 else ""),
+                       "rows_per_step": (Nt - 2) * (1 if strong else world) * K,
                        "parallelism": (f"one control, rows sharded zig-zag over {world} GPU(s) + RCCL reduce" if strong
                                        else f"{world} GPU(s), one full getHessian (own control vector) per GPU")},
             "sweep_steps_per_sec": sweep_steps / elapsed,
