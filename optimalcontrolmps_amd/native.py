@@ -283,12 +283,18 @@ class Engine:
         self._chk(lib().ocg_overlap_factor(self.h, out.ctypes.data_as(dp)), "ocg_overlap_factor")
         return complex(out[0], out[1])
 
+    def _need_N(self):
+        if self.N <= 0:
+            raise OcgError("no device trajectories yet: propagate() or hessian() first")
+
     def fidelities(self):
+        self._need_N()
         out = np.zeros(self.N)
         self._chk(lib().ocg_fidelities(self.h, out.ctypes.data_as(dp)), "ocg_fidelities")
         return out
 
     def div_t(self):
+        self._need_N()
         out = np.zeros(2 * self.N)
         self._chk(lib().ocg_div_t(self.h, out.ctypes.data_as(dp)), "ocg_div_t")
         return out.view(np.complex128).copy()
@@ -315,6 +321,7 @@ class Engine:
         as after propagate(u, 3) + xi_dH()"""
         uu, pu = _d(u)
         N = len(uu)
+        self.N = N  # the device trajectories now have N states (fidelities / div_t size their outputs by it)
         if rows is None:
             rows = range(1, N - 1)
         r, pr = _i(list(rows))
