@@ -185,6 +185,13 @@ struct Engine {
   // stats
   double gemm_flops = 0, gemm_bytes = 0, gemm_ms = 0;
   long gemm_launches = 0;
+  // OCG_GEMM_STATS=1: shape statistics of the GEMM launches, printed at destruction (diagnostic)
+  bool gstat = std::getenv("OCG_GEMM_STATS") != nullptr;
+  double gs_pad = 0, gs_flop = 0, gs_tiles_hist[6] = {0}, gs_flop_m[6] = {0}, gs_flop_k[6] = {0};
+  long gs_launch_hist[6] = {0};
+  double gs_ms[6] = {0}, gs_bflop[6] = {0}, gs_ntask[6] = {0}, gs_nseg[6] = {0}, gs_m[6] = {0}, gs_n[6] = {0}, gs_k[6] = {0};
+  std::vector<int> gs_evb;  // bucket of each pending gemm_ev pair
+  static int gs_bucket(double x) { return x < 32 ? 0 : x < 64 ? 1 : x < 128 ? 2 : x < 256 ? 3 : x < 512 ? 4 : 5; }
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gemm_ev;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_kept = nullptr;
@@ -198,6 +205,21 @@ struct Engine {
       : L(L_), p(p_), Q(npart), Q1(npart + 1), J(J_), dt(dt_), cutoff(cutoff_),
         maxm(maxm_ > 0 ? maxm_ : 5000), device(device_) {}
   ~Engine() {
+    if (gstat && gemm_launches) {
+      if (st) (void)hipStreamSynchronize(st);
+      resolve_timers();
+      std::fprintf(stderr, "[gemm] launches %ld  alg/padded flops %.3f\n", gemm_launches, gs_flop / std::max(gs_pad, 1.0));
+      const char* lb[6] = {"<32", "<64", "<128", "<256", "<512", ">=512"};
+      for (int b = 0; b < 6; ++b)
+        std::fprintf(stderr, "[gemm] %-6s launches(tiles/8) %ld  tiles %.0f  ms %.1f  TF %.2f  flop share by max(m,n) %.3f  by k %.3f\n", lb[b],
+                     gs_launch_hist[b], gs_tiles_hist[b], gs_ms[b], gs_bflop[b] / std::max(gs_ms[b], 1e-9) * 1e-9, gs_flop_m[b] / std::max(gs_flop, 1.0),
+                     gs_flop_k[b] / std::max(gs_flop, 1.0));
+      for (int b = 0; b < 6; ++b)
+        if (gs_ntask[b] > 0)
+          std::fprintf(stderr, "[gemm] %-6s tasks/launch %.1f  segs/task %.2f  avg m %.1f n %.1f k/seg %.1f\n", lb[b],
+                       gs_ntask[b] / std::max<long>(gs_launch_hist[b], 1), gs_nseg[b] / gs_ntask[b], gs_m[b] / gs_ntask[b],
+                       gs_n[b] / gs_ntask[b], gs_k[b] / std::max(gs_nseg[b], 1.0));
+    }
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& e : gemm_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (ev_kept) (void)hipEventDestroy(ev_kept);
@@ -423,16 +445,20 @@ struct Engine {
     return e;
   }
   void resolve_timers() {
-    for (auto& pr : gemm_ev) {
+    for (size_t i = 0; i < gemm_ev.size(); ++i) {
+      auto& pr = gemm_ev[i];
       float ms = 0;
       if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) gemm_ms += ms;
+      if (gstat && i < gs_evb.size()) gs_ms[gs_evb[i]] += ms;
       ev_pool.push_back(pr.first);
       ev_pool.push_back(pr.second);
     }
     gemm_ev.clear();
+    gs_evb.clear();
   }
   // GEMM tasks: drop empty outputs, prefix the tiles, account flops/bytes
   void gemm(std::vector<GTask>& tasks, const std::vector<GSeg>& segs) {
+    const double f0 = gemm_flops;
     std::vector<GTask> t;
     t.reserve(tasks.size());
     int tiles = 0;
@@ -443,6 +469,13 @@ struct Engine {
       for (int s = 0; s < x.nseg; ++s) {
         const GSeg& g = segs[x.seg0 + s];
         gemm_flops += 8.0 * x.m * x.n * g.k;
+        if (gstat) {
+          const double f = 8.0 * x.m * x.n * g.k;
+          gs_flop += f;
+          gs_pad += 8.0 * ((x.m + 31) / 32 * 32) * ((x.n + 31) / 32 * 32) * ((g.k + 3) / 4 * 4);
+          gs_flop_m[gs_bucket(std::max(x.m, x.n))] += f;
+          gs_flop_k[gs_bucket(g.k)] += f;
+        }
         gemm_bytes += 16.0 * (double(x.m) * g.k + double(g.k) * x.n);
       }
       gemm_bytes += 16.0 * x.m * x.n;
@@ -450,6 +483,20 @@ struct Engine {
     }
     tasks.clear();
     if (t.empty()) return;
+    if (gstat) {
+      const int b = gs_bucket(tiles / 8.0);
+      ++gs_launch_hist[b];
+      gs_evb.push_back(b);
+      gs_bflop[b] += gemm_flops - f0;
+      gs_ntask[b] += t.size();
+      for (auto& x : t) {
+        gs_nseg[b] += x.nseg;
+        gs_m[b] += x.m;
+        gs_n[b] += x.n;
+        for (int q = 0; q < x.nseg; ++q) gs_k[b] += segs[x.seg0 + q].k;
+      }
+      gs_tiles_hist[b] += tiles;
+    }
     const GTask* dt_ = upload(t);
     const GSeg* ds = upload(segs);
     hipEvent_t a = get_event(), b = get_event();

@@ -107,13 +107,17 @@ __device__ __forceinline__ int find_task(const T* tasks, int ntask, long long e,
 // ------------------------------------------------------------------ GEMM
 // One workgroup = one 32x32 tile of one task; wave w owns the 16x16 sub-tile
 // (w >> 1, w & 1).  K is staged through LDS in chunks of 16 (re and im planes
-// separately, padded), each chunk feeds 4 k-steps of 4 complex MFMA groups:
+// separately, padded; the next chunk's global loads are in flight while the
+// current one feeds the MFMAs), each chunk feeds up to 4 k-steps of 4 complex
+// MFMA groups (k-steps past the segment's k are skipped):
 //   re += a.re b.re - a.im b.im,  im += a.re b.im + a.im b.re
 // (v_mfma_f64_16x16x4f64 operands: lane l holds A[l & 15][k = l >> 4] and
 // B[k = l >> 4][l & 15]; results col = l & 15, row = (l >> 4) + 4 r).
+// (GK 32 and 64 measured slower on the config-4 mix: fewer workgroups per CU.)
 constexpr int GT = 32, GK = 16;
 __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, int ntask,
                                              const GSeg* __restrict__ segs) {
+  constexpr int EA = GT * GK / NT;  // staged elements per thread and operand
   __shared__ double Ar[GT][GK + 1], Ai[GT][GK + 1], Br[GK][GT + 1], Bi[GK][GT + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ti = find_task(tasks, ntask, (long long)blockIdx.x, [](const GTask& t) { return (long long)t.tile0; });
@@ -126,14 +130,15 @@ __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, in
   for (int s = 0; s < T.nseg; ++s) {
     const GSeg S = segs[T.seg0 + s];
     const bool ca = S.ops & 1, cb = (S.ops >> 1) & 1;
-    for (int k0 = 0; k0 < S.k; k0 += GK) {
-      // stage op(A)[m0.., k0..] (32 x 16) and op(B)[k0.., n0..] (16 x 32)
+    // global -> registers for the chunk at k0 (issued one chunk ahead of its MFMAs)
+    z va[EA], vb[EA];
+    auto gload = [&](int k0) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < EA; ++t) {
         const int e = tid + NT * t;
         int r, kk;
-        if (!ca) { r = e >> 4; kk = e & 15; }
-        else { kk = e >> 5; r = e & 31; }
+        if (!ca) { r = e / GK; kk = e % GK; }
+        else { kk = e / GT; r = e % GT; }
         z v = mk(0, 0);
         const int gr = m0 + r, gk = k0 + kk;
         if (gr < T.m && gk < S.k) {
@@ -141,34 +146,49 @@ __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, in
           if (ca) v.y = -v.y;
           v = zsc(v, S.alpha);
         }
-        Ar[r][kk] = v.x;
-        Ai[r][kk] = v.y;
+        va[t] = v;
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < EA; ++t) {
         const int e = tid + NT * t;
         int kk, c;
-        if (!cb) { kk = e >> 5; c = e & 31; }
-        else { c = e >> 4; kk = e & 15; }
+        if (!cb) { kk = e / GT; c = e % GT; }
+        else { c = e / GK; kk = e % GK; }
         z v = mk(0, 0);
         const int gc = n0 + c, gk = k0 + kk;
         if (gc < T.n && gk < S.k) {
           v = cb ? S.B[(size_t)gc * S.ldb + gk] : S.B[(size_t)gk * S.ldb + gc];
           if (cb) v.y = -v.y;
         }
-        Br[kk][c] = v.x;
-        Bi[kk][c] = v.y;
+        vb[t] = v;
+      }
+    };
+    if (S.k > 0) gload(0);
+    for (int k0 = 0; k0 < S.k; k0 += GK) {
+      // stage op(A)[m0.., k0..] (32 x GK) and op(B)[k0.., n0..] (GK x 32)
+#pragma unroll
+      for (int t = 0; t < EA; ++t) {
+        const int e = tid + NT * t;
+        const int r = !ca ? e / GK : e % GT, kk = !ca ? e % GK : e / GT;
+        Ar[r][kk] = va[t].x;
+        Ai[r][kk] = va[t].y;
+        const int kb = !cb ? e / GT : e % GK, c = !cb ? e % GT : e / GK;
+        Br[kb][c] = vb[t].x;
+        Bi[kb][c] = vb[t].y;
       }
       __syncthreads();
+      if (k0 + GK < S.k) gload(k0 + GK);
 #pragma unroll
       for (int ks = 0; ks < GK; ks += 4) {
-        const int ar = wm + (lane & 15), kk = ks + (lane >> 4), bc = wn + (lane & 15);
-        const double are = Ar[ar][kk], aim = Ai[ar][kk];
-        const double bre = Br[kk][bc], bim = Bi[kk][bc];
-        cr = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bre, cr, 0, 0, 0);
-        cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-aim, bim, cr, 0, 0, 0);
-        ci = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bim, ci, 0, 0, 0);
-        ci = __builtin_amdgcn_mfma_f64_16x16x4f64(aim, bre, ci, 0, 0, 0);
+        if (k0 + ks < S.k) {  // k-steps past the end would only add zeros
+          const int ar = wm + (lane & 15), kk = ks + (lane >> 4), bc = wn + (lane & 15);
+          const double are = Ar[ar][kk], aim = Ai[ar][kk];
+          const double bre = Br[kk][bc], bim = Bi[kk][bc];
+          cr = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bre, cr, 0, 0, 0);
+          cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-aim, bim, cr, 0, 0, 0);
+          ci = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bim, ci, 0, 0, 0);
+          ci = __builtin_amdgcn_mfma_f64_16x16x4f64(aim, bre, ci, 0, 0, 0);
+        }
       }
       __syncthreads();
     }
