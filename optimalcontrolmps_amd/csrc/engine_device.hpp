@@ -1139,6 +1139,7 @@ struct Chain {
         g = valid ? zc(Gc[loc]) : c2(0.0, 0.0);
         w = valid ? zc(Wc[loc]) : c2(i == j ? 1.0 : 0.0, 0.0);
       }
+      pf(14);  // profile: Gram formation above (jacobi A), rounds below (jacobi B)
       // per-round roles: partners of i and j (idle / padded: self), the
       // bpermute addresses of the two rotations and three partner elements
       int arow[MR], acol[MR], aipj[MR], apij[MR], apipj[MR], fl[MR];

@@ -717,6 +717,20 @@ struct Engine {
     // eigenvectors of the kept eigenvalues (reads the kept counts on the device)
     hipLaunchKernelGGL(k_heev_vecs_reg, dim3(np), dim3(VNT), 0, st, R.d_probs, np);
     HCK(hipGetLastError());
+    {
+      // back-transformation of the larger problems (kept counts known on the device only:
+      // every 16-column block a problem of this order could keep; the others exit at once)
+      std::vector<int2> bt;
+      for (int i = 0; i < np; ++i) {
+        const int n = R.probs[i].n;
+        if (n > 64 && n <= kBtRows)
+          for (int cb = 0; 16 * cb < n; ++cb) bt.push_back(make_int2(i, cb));
+      }
+      if (!bt.empty()) {
+        hipLaunchKernelGGL(k_heev_bt, dim3(int(bt.size())), dim3(BNT), 0, st, R.d_probs, upload(bt));
+        HCK(hipGetLastError());
+      }
+    }
     HCK(hipEventSynchronize(ev_kept));
     for (size_t j = 0; j < jobs.size(); ++j) {
       jobs[j].kept.assign(Q1, 0);

@@ -542,6 +542,14 @@ __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const 
   }
 }
 
+// problems whose eigenvectors the vecs kernel finishes itself (Z in LDS, U in registers)
+__device__ __forceinline__ bool vecs_fast(int n, int k) {
+  return n <= RNMAX && k <= 64 && (size_t(n) * (k + 1) + size_t(n) + 64 * 65) * 8 <= size_t(kVecLds);
+}
+// the others of order <= kBtRows leave Z (ld n) in P.Z for k_heev_bt
+constexpr int kBtRows = 512;
+constexpr int BNT = 256;  // threads of k_heev_bt (one wave per SIMD: 32 rows x 2 complex per lane in VGPRs)
+constexpr int kBtBlk = 16;  // reflectors per LDS block (16 x 512 complex = 128 KB)
 constexpr int kVecRows = (RNMAX + VNT / 64 - 1) / (VNT / 64);  // rows per thread (fast path)
 constexpr int kRefBlk = 24;                   // reflectors per LDS block
 
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
     return;
   }
   const int ldz = k + 1;  // odd stride: row reads of Z by consecutive threads hit distinct banks
-  const bool fast = n <= RNMAX && k <= 64 && (size_t(n) * ldz + size_t(n) + 64 * 65) * 8 <= size_t(kVecLds);
+  const bool fast = vecs_fast(n, k);
   double* Zl = (double*)un;
   // generic path: the tridiagonal in global memory scratch (P.d / P.e), Z and U global
   const double* Gd = P.d;
@@ -751,6 +759,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
     }
   }
   STAMP(1);
+  if (!fast && n <= kBtRows) return;  // U = Q D Z by k_heev_bt
   if (!fast) {
     // U = Q D Z in global memory, reflectors j = n-2 .. 0 (one column per thread)
     z* U = P.U;
@@ -771,6 +780,11 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
       }
       __syncthreads();
     }
+    STAMP(4);
+#ifdef HBM_STAMP
+    if (tid == 0)
+      for (int q = 0; q < 8; ++q) P.Z[q] = double(stamp_acc[q]);
+#endif
     return;
   }
   // ---- fast path: U in registers.  Lane l of wave w: row chunk rc = l >> 2
@@ -854,6 +868,83 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
       const int i = 16 * t + rc;
       if (i < n) P.U[(size_t)i * k + col] = Ur[g][t];
     }
+  }
+}
+
+// ------------------------------------------------------------------ back-transformation
+// U = Q D Z for the problems the vecs kernel left in global memory (order
+// kBtRows at most, not vecs_fast): one workgroup per (problem, block of 16
+// kept columns).  Lane l of wave w holds column 16 cb + 4 w + (l & 3), rows
+// i = 16 t + (l >> 2) (t < 32) in registers; the reflectors j = n-2 .. 0 are
+// staged through LDS kBtBlk at a time and applied with in-wave reductions over
+// the 16 row chunks, as in the vecs kernel's fast path.  tasks: (problem,
+// column block); blocks past the problem's kept count exit at once.
+__global__ __launch_bounds__(BNT) void k_heev_bt(const EProb* __restrict__ probs, const int2* __restrict__ tasks) {
+  __shared__ z Rb[kBtBlk * kBtRows];
+  __shared__ double stau[kBtBlk];
+  const int2 tk = tasks[blockIdx.x];
+  const EProb P = probs[tk.x];
+  const int n = P.n;
+  if (n <= 1 || n > kBtRows) return;
+  const int k = *P.kept;
+  if (k <= 0 || vecs_fast(n, k)) return;
+  const int c0 = 16 * tk.y;
+  if (c0 >= k) return;  // workgroup-uniform
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int rc = lane >> 2, col = c0 + 4 * wv + (lane & 3);
+  const bool wave_live = c0 + 4 * wv < k;  // wave-uniform
+  constexpr int TR = kBtRows / 16;
+  z Ur[TR];
+#pragma unroll
+  for (int t = 0; t < TR; ++t) {
+    const int i = 16 * t + rc;
+    Ur[t] = (i < n && col < k) ? zsc(P.ph[i], P.Z[(size_t)i * n + col]) : mk(0, 0);
+  }
+  for (int jhi = n - 2; jhi >= 0; jhi -= kBtBlk) {
+    const int jlo = jhi - kBtBlk + 1 > 0 ? jhi - kBtBlk + 1 : 0;
+    const int nb = jhi - jlo + 1;
+    __syncthreads();  // previous block consumed
+    for (int e = tid; e < nb * n; e += BNT) {
+      const int rr = e / nb, jj = e - rr * nb, j = jlo + jj;
+      Rb[jj * kBtRows + rr] = rr > j ? P.A[(size_t)rr * n + j] : mk(0, 0);
+    }
+    for (int jj = tid; jj < nb; jj += BNT) stau[jj] = P.tau[jlo + jj];
+    __syncthreads();
+    if (!wave_live) continue;
+    for (int j = jhi; j >= jlo; --j) {
+      const double t = stau[j - jlo];
+      if (t == 0.0) continue;  // uniform
+      const z* u = Rb + (j - jlo) * kBtRows;
+      const int t0 = (j + 1) >> 4;  // first row slot holding rows > j (uniform)
+      z uu[TR];
+#pragma unroll
+      for (int tt = 0; tt < TR; ++tt) uu[tt] = (tt >= t0 && 16 * tt + rc < n) ? u[16 * tt + rc] : mk(0, 0);
+      z sacc = mk(0, 0);
+#pragma unroll
+      for (int tt = 0; tt < TR; ++tt) {
+        if (tt < t0) continue;
+        sacc.x = fma(uu[tt].x, Ur[tt].x, fma(uu[tt].y, Ur[tt].y, sacc.x));  // conj(u) U
+        sacc.y = fma(uu[tt].x, Ur[tt].y, fma(-uu[tt].y, Ur[tt].x, sacc.y));
+      }
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) {
+        sacc.x += __shfl_xor(sacc.x, o, 64);
+        sacc.y += __shfl_xor(sacc.y, o, 64);
+      }
+      sacc = zsc(sacc, t);
+#pragma unroll
+      for (int tt = 0; tt < TR; ++tt) {
+        if (tt < t0) continue;
+        Ur[tt].x = fma(-uu[tt].x, sacc.x, fma(uu[tt].y, sacc.y, Ur[tt].x));
+        Ur[tt].y = fma(-uu[tt].x, sacc.y, fma(-uu[tt].y, sacc.x, Ur[tt].y));
+      }
+    }
+  }
+  if (col >= k) return;
+#pragma unroll
+  for (int t = 0; t < TR; ++t) {
+    const int i = 16 * t + rc;
+    if (i < n) P.U[(size_t)i * k + col] = Ur[t];
   }
 }
 

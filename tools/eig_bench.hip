@@ -64,6 +64,15 @@ int main(int argc, char** argv) {
   int* didx;
   CK(hipMalloc(&didx, 4 * B));
   CK(hipMemcpy(didx, idx.data(), 4 * B, hipMemcpyHostToDevice));
+  std::vector<int2> bt;
+  for (int b = 0; b < B; ++b)
+    if (n > 64 && n <= kBtRows)
+      for (int cb = 0; 16 * cb < n; ++cb) bt.push_back(make_int2(b, cb));
+  int2* dbt = nullptr;
+  if (!bt.empty()) {
+    CK(hipMalloc(&dbt, sizeof(int2) * bt.size()));
+    CK(hipMemcpy(dbt, bt.data(), sizeof(int2) * bt.size(), hipMemcpyHostToDevice));
+  }
   hipEvent_t e0, e1, e2;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
   double tv = 0, tvec = 0;
@@ -76,6 +85,7 @@ int main(int argc, char** argv) {
     }
     CK(hipEventRecord(e1));
     hipLaunchKernelGGL(k_heev_vecs_reg, dim3(B), dim3(VNT), 0, 0, dP, B);
+    if (dbt) hipLaunchKernelGGL(k_heev_bt, dim3(int(bt.size())), dim3(BNT), 0, 0, dP, dbt);
     CK(hipEventRecord(e2));
     CK(hipEventSynchronize(e2));
     float a, b2;

@@ -8,7 +8,8 @@ if not os.path.exists(lib) or "--rebuild" in sys.argv:  # build on the CPU side 
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                            "-DOCG_PROFILE", f"-DOCG_NT={NT}", "-o", lib,
-                           os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip")])
+                           os.path.join(ROOT, "optimalcontrolmps_amd/csrc/ocmps.hip"),
+                           os.path.join(ROOT, "optimalcontrolmps_amd/csrc/hbm.hip")])
 if "--build-only" in sys.argv:
     sys.exit(0)
 print(f"NT = {NT}")
