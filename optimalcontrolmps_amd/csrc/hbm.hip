@@ -197,6 +197,9 @@ struct Engine {
   hipEvent_t ev_kept = nullptr;
   // smallest Gram order on the register eigensolver (OCG_HBM_REGMIN overrides: A/B and tests)
   int reg_min = kRegMin;
+  // smallest Gram order on the blocked kernel k_heev_vals_big (default: the orders the register
+  // kernels cannot hold); OCG_HBM_BIGMIN overrides (tests; > kBigMax: the eager L2 kernel, A/B)
+  int big_min = std::getenv("OCG_HBM_BIGMIN") ? std::atoi(std::getenv("OCG_HBM_BIGMIN")) : RNMAX + 1;
   double phase_ms[8] = {0};
   long phase_n[8] = {0};
   double steps_done[8] = {0};
@@ -693,17 +696,26 @@ struct Engine {
     {
       // one launch: per block the register variant for its order (or the LDS / L2
       // kernel), largest blocks first; dynamic LDS = max over the variants present
-      std::vector<int> order(np);
-      for (int i = 0; i < np; ++i) order[i] = i;
+      // orders big_min <= n <= kBigMax: the blocked reduction (k_heev_vals_big)
+      std::vector<int> order, big;
+      for (int i = 0; i < np; ++i) (R.probs[i].n >= std::max(big_min, 2) && R.probs[i].n <= kBigMax ? big : order).push_back(i);
       std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
+      std::stable_sort(big.begin(), big.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
+      if (!big.empty()) {
+        hipLaunchKernelGGL(k_heev_vals_big, dim3(int(big.size())), dim3(VBG), 0, st, R.d_probs, upload(big));
+        HCK(hipGetLastError());
+      }
       int lds_v = 64;
-      for (int i = 0; i < np; ++i) {
+      for (int i : order) {
         const int n = R.probs[i].n;
         lds_v = std::max(lds_v, (n >= reg_min && n <= RNMAX) ? reg_lds_bytes(reg_grid(n))
                                                               : 64 * n + (n <= kLdsOrder ? 16 * n * n : 0) + 64);
       }
-      hipLaunchKernelGGL(k_heev_vals_any, dim3(np), dim3(RNT), lds_v, st, R.d_probs, upload(order), reg_min);
-      HCK(hipGetLastError());
+      if (!order.empty()) {
+        hipLaunchKernelGGL(k_heev_vals_any, dim3(int(order.size())), dim3(RNT), lds_v, st, R.d_probs, upload(order),
+                           reg_min);
+        HCK(hipGetLastError());
+      }
     }
     int maxnp = 0;
     for (auto& I : items) maxnp = std::max(maxnp, I.np);

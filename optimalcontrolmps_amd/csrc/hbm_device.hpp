@@ -433,6 +433,65 @@ __device__ __forceinline__ int sturm(const double* d, const double* e2, int n, d
   return c;
 }
 
+// From the reduced tridiagonal (diagonal in Ld, complex subdiagonal beta in LB):
+// the phases making it real (P.ph), d / e (P.d, P.e), and every eigenvalue by
+// bisection (thread t -> the t-th largest), for an NTH-thread workgroup.
+template <int NTH>
+__device__ __forceinline__ void vals_from_tridiag(const EProb& P, int n, double* Ld, double* Le2, const z* LB) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if (tid == 0) {
+    z dl = mk(1, 0);
+    P.ph[0] = dl;
+    for (int j = 0; j + 1 < n; ++j) {
+      const z b = LB[j];
+      const double ab = sqrt(b.x * b.x + b.y * b.y);
+      if (ab > 0) dl = zmul(dl, mk(b.x / ab, b.y / ab));
+      P.ph[j + 1] = dl;
+      P.e[j] = ab;
+      Le2[j] = ab * ab;
+    }
+    P.e[n - 1] = 0;
+    Le2[n - 1] = 0;
+  }
+  for (int j = tid; j < n; j += NTH) P.d[j] = Ld[j];
+  __syncthreads();
+  // Gershgorin bounds, pivmin (LAPACK dstebz conventions)
+  double gl = 1e300, gu = -1e300, emax = 0;
+  for (int i = tid; i < n; i += NTH) {
+    const double el = i > 0 ? sqrt(Le2[i - 1]) : 0.0, er = i + 1 < n ? sqrt(Le2[i]) : 0.0;
+    gl = fmin(gl, Ld[i] - el - er);
+    gu = fmax(gu, Ld[i] + el + er);
+    emax = fmax(emax, Le2[i]);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    gl = fmin(gl, __shfl_xor(gl, o, 64));
+    gu = fmax(gu, __shfl_xor(gu, o, 64));
+    emax = fmax(emax, __shfl_xor(emax, o, 64));
+  }
+  __shared__ double bb[3][NTH / 64];
+  if ((tid & 63) == 0) { bb[0][tid >> 6] = gl; bb[1][tid >> 6] = gu; bb[2][tid >> 6] = emax; }
+  __syncthreads();
+  gl = bb[0][0]; gu = bb[1][0]; emax = bb[2][0];
+  for (int i = 1; i < NTH / 64; ++i) { gl = fmin(gl, bb[0][i]); gu = fmax(gu, bb[1][i]); emax = fmax(emax, bb[2][i]); }
+  const double eps = 2.220446049250313e-16, safmin = 2.2250738585072014e-308;
+  const double tnorm = fmax(fabs(gl), fabs(gu));
+  const double pivmin = safmin * fmax(1.0, emax);
+  gl -= 2.0 * eps * tnorm * n + 2.0 * pivmin;
+  gu += 2.0 * eps * tnorm * n + 2.0 * pivmin;
+  const double atol = 4.0 * eps * tnorm;
+  for (int t = tid; t < n; t += NTH) {
+    const int idx = n - 1 - t;  // ascending index of the t-th largest
+    double lo = gl, hi = gu;
+    for (int it = 0; it < 128 && hi - lo > atol + 2.0 * eps * fmax(fabs(lo), fabs(hi)); ++it) {
+      const double mid = 0.5 * (lo + hi);
+      if (sturm(Ld, Le2, n, mid, pivmin) > idx) hi = mid;
+      else lo = mid;
+    }
+    P.w[t] = 0.5 * (lo + hi);
+  }
+}
+
 // eigenvalues: tridiagonalise (in LDS for small orders), make the tridiagonal
 // real, bisect every eigenvalue (thread t -> the t-th largest)
 __device__ __forceinline__ void heev_vals_lds_body(const EProb& P, char* smem) {
@@ -467,57 +526,7 @@ __device__ __forceinline__ void heev_vals_lds_body(const EProb& P, char* smem) {
     __syncthreads();
     for (int e = tid; e < n * n; e += NT) P.A[e] = A[e];
   }
-  __syncthreads();
-  if (tid == 0) {
-    z dl = mk(1, 0);
-    P.ph[0] = dl;
-    for (int j = 0; j + 1 < n; ++j) {
-      const z b = LB[j];
-      const double ab = sqrt(b.x * b.x + b.y * b.y);
-      if (ab > 0) dl = zmul(dl, mk(b.x / ab, b.y / ab));
-      P.ph[j + 1] = dl;
-      P.e[j] = ab;
-      Le2[j] = ab * ab;
-    }
-    P.e[n - 1] = 0;
-    Le2[n - 1] = 0;
-  }
-  for (int j = tid; j < n; j += NT) P.d[j] = Ld[j];
-  __syncthreads();
-  // Gershgorin bounds, pivmin (LAPACK dstebz conventions)
-  double gl = 1e300, gu = -1e300, emax = 0;
-  for (int i = tid; i < n; i += NT) {
-    const double el = i > 0 ? sqrt(Le2[i - 1]) : 0.0, er = i + 1 < n ? sqrt(Le2[i]) : 0.0;
-    gl = fmin(gl, Ld[i] - el - er);
-    gu = fmax(gu, Ld[i] + el + er);
-    emax = fmax(emax, Le2[i]);
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    gl = fmin(gl, __shfl_xor(gl, o, 64));
-    gu = fmax(gu, __shfl_xor(gu, o, 64));
-    emax = fmax(emax, __shfl_xor(emax, o, 64));
-  }
-  __shared__ double bb[3][NT / 64];
-  if ((tid & 63) == 0) { bb[0][tid >> 6] = gl; bb[1][tid >> 6] = gu; bb[2][tid >> 6] = emax; }
-  __syncthreads();
-  gl = bb[0][0]; gu = bb[1][0]; emax = bb[2][0];
-  for (int i = 1; i < NT / 64; ++i) { gl = fmin(gl, bb[0][i]); gu = fmax(gu, bb[1][i]); emax = fmax(emax, bb[2][i]); }
-  const double eps = 2.220446049250313e-16, safmin = 2.2250738585072014e-308;
-  const double tnorm = fmax(fabs(gl), fabs(gu));
-  const double pivmin = safmin * fmax(1.0, emax);
-  gl -= 2.0 * eps * tnorm * n + 2.0 * pivmin;
-  gu += 2.0 * eps * tnorm * n + 2.0 * pivmin;
-  const double atol = 4.0 * eps * tnorm;
-  for (int t = tid; t < n; t += NT) {
-    const int idx = n - 1 - t;  // ascending index of the t-th largest
-    double lo = gl, hi = gu;
-    for (int it = 0; it < 128 && hi - lo > atol + 2.0 * eps * fmax(fabs(lo), fabs(hi)); ++it) {
-      const double mid = 0.5 * (lo + hi);
-      if (sturm(Ld, Le2, n, mid, pivmin) > idx) hi = mid;
-      else lo = mid;
-    }
-    P.w[t] = 0.5 * (lo + hi);
-  }
+  vals_from_tridiag<NT>(P, n, Ld, Le2, LB);
 }
 
 __device__ __forceinline__ double hrand(unsigned i, unsigned j) {

@@ -948,4 +948,290 @@ __global__ __launch_bounds__(BNT) void k_heev_bt(const EProb* __restrict__ probs
   }
 }
 
+// ------------------------------------------------------------------ large orders
+// Eigenvalues of Gram blocks of order RNMAX < n <= kBigMax (config 5's sectors
+// at chi = 512): the lower triangle no longer fits one CU's registers, and the
+// eager L2 reduction (tridiag) reads and writes the trailing matrix three times
+// per column.  Here the reduction is blocked like LAPACK's zhetrd / zlatrd:
+// inside a panel of BNB columns the stored trailing matrix stays stale and its
+// pending updates are carried by the panel vectors (A_j = A - U W^H - W U^H):
+// thread r keeps row r of U and W in registers, so the pending updates of the
+// column being reduced and of the matrix-vector product cost no memory
+// traffic; one rank-2 BNB update of the trailing block (rows staged through
+// the problem's Z / Dv scratch and LDS) closes the panel.  Per column the
+// trailing matrix is read once (the product, 64 columns per wave, split over
+// up to 8 row chunks).  Same reflector conventions as tridiag (vector j in
+// column j of A, u[j+1] = u0, tau real), so the vecs / back-transformation
+// kernels follow unchanged; all reductions in a fixed order.
+// wave64 sum of a double: DPP within rows of 16 (xor 1, xor 2, half mirror,
+// mirror), then the four row sums by readlane; fixed order, every lane the same
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(int(b), l), hi = __builtin_amdgcn_readlane(int(b >> 32), l);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+constexpr int VBG = 512;
+constexpr int kBigMax = VBG;  // one row per thread
+constexpr int BNB = 12;
+__global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__ probs, const int* __restrict__ idx) {
+  constexpr int NWV = VBG / 64;
+  __shared__ z LU[kBigMax], LP[kBigMax], LB[kBigMax];
+  __shared__ double Ld[kBigMax], Le2[kBigMax];
+  __shared__ z rowU[BNB], rowW[BNB], dots[2 * BNB], dpart[NWV][2 * BNB];
+  __shared__ double red[NWV], scal[4];
+  __shared__ __align__(16) z ws[8 * kBigMax];  // product partials [8][kBigMax] | panel staging [4][64][BNB]
+  static_assert(4 * 64 * BNB <= 8 * kBigMax, "panel staging fits the partials region");
+  const EProb P = probs[idx[blockIdx.x]];
+  const int n = P.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (n < 2 || n > kBigMax) return;
+  z* A = P.A;
+  z* U = reinterpret_cast<z*>(P.Z);  // n x BNB (ld BNB): panel rows for the closing update
+  z* W = reinterpret_cast<z*>(P.Dv);
+  const int r = tid;  // this thread's row
+  z pu[BNB], pw[BNB];  // row r of the panel's U and W
+#ifdef HBM_STAMP
+  unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
+#endif
+  auto bsum = [&](double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (lane == 0) red[wv] = v;
+    __syncthreads();
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < NWV; ++i) s += red[i];
+    return s;
+  };
+  for (int p0 = 0; p0 < n - 1; p0 += BNB) {
+    const int pe = p0 + BNB < n - 1 ? p0 + BNB : n - 1;
+#pragma unroll
+    for (int q = 0; q < BNB; ++q) { pu[q] = mk(0, 0); pw[q] = mk(0, 0); }
+    for (int j = p0; j < pe; ++j) {
+      const int l = j - p0, m = n - j - 1;
+      if (r == j) {
+#pragma unroll
+        for (int q = 0; q < BNB; ++q) { rowU[q] = pu[q]; rowW[q] = pw[q]; }
+      }
+      __syncthreads();
+      // column j (rows j..n-1) with the panel's pending updates
+      if (r >= j && r < n) {
+        z x = A[(size_t)r * n + j];
+#pragma unroll
+        for (int q = 0; q < BNB; ++q)  // slots q >= l hold zeros: exact no-ops, no branches
+          x = zsub(x, zadd(zmul(pu[q], zcj(rowW[q])), zmul(pw[q], zcj(rowU[q]))));
+        if (r == j) Ld[j] = x.x;
+        else LU[r - j - 1] = x;
+      }
+      __syncthreads();
+      STAMP(0);
+      // reflector H = I - t u u^H zeroing x[1..m)
+      double s = 0;
+      for (int i = 1 + tid; i < m; i += VBG) s += LU[i].x * LU[i].x + LU[i].y * LU[i].y;
+      s = bsum(s);
+      if (tid == 0) {
+        const z a = LU[0];
+        const double aa = sqrt(a.x * a.x + a.y * a.y), xn = sqrt(aa * aa + s);
+        double t = 0;
+        z b = mk(0, 0), u0 = a;
+        if (xn > 0) {
+          const z ph = aa > 0 ? mk(a.x / aa, a.y / aa) : mk(1, 0);
+          b = mk(-ph.x * xn, -ph.y * xn);
+          u0 = mk(a.x + ph.x * xn, a.y + ph.y * xn);
+          const double ua = aa + xn;
+          t = 2.0 / (ua * ua + s);
+        }
+        P.tau[j] = t;
+        LB[j] = b;
+        scal[0] = t;
+        scal[1] = u0.x;
+        scal[2] = u0.y;
+      }
+      __syncthreads();
+      const double t = scal[0];
+      if (t == 0.0) continue;  // column already reduced: H = I, panel slot l stays zero
+      if (tid == 0) LU[0] = mk(scal[1], scal[2]);
+      __syncthreads();
+      STAMP(1);
+      const bool mine = r > j && r < n;  // this thread's row is in the trailing block
+      const z ur = mine ? LU[r - j - 1] : mk(0, 0);
+      if (mine) A[(size_t)r * n + j] = ur;  // reflector j in column j
+      // p = A_t u on the stored (panel-stale) trailing matrix: wave (ib, kc)
+      // sums rows of chunk kc for columns 64 ib + lane; p_i = sum_k conj(A[k][i]) u_k
+      const int nib = (m + 63) >> 6;
+      const int kch = NWV / nib < 1 ? 1 : NWV / nib;
+      for (int task = wv; task < nib * kch; task += NWV) {
+        const int ib = task % nib, kc = task / nib;
+        const int i = 64 * ib + lane;
+        if (i < m) {
+          const int klen = (m + kch - 1) / kch, k0 = kc * klen, k1 = k0 + klen < m ? k0 + klen : m;
+          const z* col = A + (size_t)(j + 1) * n + (j + 1) + i;
+          z acc = mk(0, 0);
+          int k = k0;
+          for (; k + 7 < k1; k += 8) {
+            z av[8];
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) av[tt] = col[(size_t)(k + tt) * n];
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) {
+              const z uk = LU[k + tt];
+              acc.x += av[tt].x * uk.x + av[tt].y * uk.y;
+              acc.y += av[tt].x * uk.y - av[tt].y * uk.x;
+            }
+          }
+          for (; k < k1; ++k) {
+            const z av = col[(size_t)k * n], uk = LU[k];
+            acc.x += av.x * uk.x + av.y * uk.y;
+            acc.y += av.x * uk.y - av.y * uk.x;
+          }
+          ws[kc * kBigMax + i] = acc;
+        }
+      }
+      STAMP(2);
+      // panel dots: dots[q] = W_q^H u, dots[BNB + q] = U_q^H u (rows j+1..n-1; zero rows elsewhere)
+      {
+        // the l filled slots: wave sums by DPP + readlane, no LDS traffic
+#pragma unroll
+        for (int q = 0; q < BNB; ++q) {
+          if (q >= l) continue;  // uniform
+          const z a = zcjmul(pw[q], ur), b = zcjmul(pu[q], ur);
+          const double ax = wave_sum_dpp(a.x), ay = wave_sum_dpp(a.y);
+          const double bx = wave_sum_dpp(b.x), by = wave_sum_dpp(b.y);
+          if (lane == 0) {
+            dpart[wv][q] = mk(ax, ay);
+            dpart[wv][BNB + q] = mk(bx, by);
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < 2 * BNB) {
+        z a = mk(0, 0);
+        if ((tid < BNB ? tid : tid - BNB) < l)
+#pragma unroll
+          for (int w = 0; w < NWV; ++w) a = zadd(a, dpart[w][tid]);
+        dots[tid] = a;  // slots past l: zero
+      }
+      __syncthreads();
+      STAMP(3);
+      // p = t (A u - U (W^H u) - W (U^H u));  K = t/2 Re(u^H p);  w = p - K u
+      double kk = 0;
+      z p = mk(0, 0);
+      if (mine) {
+        const int i = r - j - 1;
+        p = ws[i];
+        for (int c = 1; c < kch; ++c) p = zadd(p, ws[c * kBigMax + i]);
+#pragma unroll
+        for (int q = 0; q < BNB; ++q) p = zsub(p, zadd(zmul(pu[q], dots[q]), zmul(pw[q], dots[BNB + q])));
+        p = zsc(p, t);
+        kk = ur.x * p.x + ur.y * p.y;
+      }
+      kk = 0.5 * t * bsum(kk);
+      const z wr = zsub(p, zsc(ur, kk));
+#pragma unroll
+      for (int q = 0; q < BNB; ++q)
+        if (q == l && mine) { pu[q] = ur; pw[q] = wr; }
+      // (the next step's first barrier orders the ws / LU reuse)
+      STAMP(4);
+    }
+    // close the panel: A[pe.., pe..] -= U W^H + W U^H (64 x 64 tiles, panel rows staged in LDS)
+    const int nl = pe - p0, mt = n - pe;
+    if (r >= pe && r < n) {
+#pragma unroll
+      for (int q = 0; q < BNB; ++q) { U[(size_t)r * BNB + q] = pu[q]; W[(size_t)r * BNB + q] = pw[q]; }
+    }
+    z* S = ws;  // [4][64][BNB]: U rows r, W rows r, U rows c, W rows c
+    // C -= [U_r W_r] [W_c U_c]^H on v_mfma_f64_16x16x4f64 (K = 2 BNB, zero-padded past nl):
+    // wave w owns the 16 x 16 tiles (w >> 1, 2 (w & 1) + {0, 1}) of the 64 x 64 block
+    const int tr = wv >> 1, tc0 = 2 * (wv & 1), ml = lane & 15, kl = lane >> 4;
+    for (int r0 = 0; r0 < mt; r0 += 64)
+      for (int c0 = 0; c0 < mt; c0 += 64) {
+        __syncthreads();
+        for (int e = tid; e < 4 * 64 * BNB; e += VBG) {
+          const int which = e / (64 * BNB), rem = e - which * (64 * BNB), row_l = rem / BNB, q = rem - row_l * BNB;
+          const int row = pe + (which < 2 ? r0 : c0) + row_l;
+          S[e] = (q < nl && row < n) ? ((which & 1) ? W : U)[(size_t)row * BNB + q] : mk(0, 0);
+        }
+        __syncthreads();
+        if (r0 + 16 * tr >= mt) continue;  // wave-uniform: tile rows past the block
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tc = tc0 + h;
+          if (c0 + 16 * tc >= mt) continue;  // wave-uniform
+          d4 cr = {0, 0, 0, 0}, ci = {0, 0, 0, 0};
+#pragma unroll
+          for (int ks = 0; ks < 2 * BNB / 4; ++ks) {
+            const int kap = 4 * ks + kl;  // this lane's k
+            const int rowA = 16 * tr + ml, colB = 16 * tc + ml;
+            const z av = kap < BNB ? S[rowA * BNB + kap] : S[(64 + rowA) * BNB + kap - BNB];
+            const z bw = kap < BNB ? S[(192 + colB) * BNB + kap] : S[(128 + colB) * BNB + kap - BNB];
+            const double bx = bw.x, by = -bw.y;  // B = conj(.)
+            cr = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bx, cr, 0, 0, 0);
+            cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, by, cr, 0, 0, 0);
+            ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, by, ci, 0, 0, 0);
+            ci = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bx, ci, 0, 0, 0);
+          }
+          const int c = pe + c0 + 16 * tc + ml;
+          if (c < n) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int rg = pe + r0 + 16 * tr + kl + 4 * rr;
+              if (rg < n) {
+                z* ap = A + (size_t)rg * n + c;
+                const z v = *ap;
+                *ap = mk(v.x - cr[rr], v.y - ci[rr]);
+              }
+            }
+          }
+        }
+      }
+    __syncthreads();
+    STAMP(5);
+  }
+  if (tid == 0) Ld[n - 1] = A[(size_t)(n - 1) * n + (n - 1)].x;
+  __syncthreads();
+  // real tridiagonal (phases P.ph, d, e) and the eigenvalues by multisection,
+  // unresolved below thr_rel * trace like the register kernels
+  if (tid == 0) {
+    z dl = mk(1, 0);
+    P.ph[0] = dl;
+    for (int j = 0; j + 1 < n; ++j) {
+      const z b = LB[j];
+      const double ab = sqrt(b.x * b.x + b.y * b.y);
+      if (ab > 0) dl = zmul(dl, mk(b.x / ab, b.y / ab));
+      P.ph[j + 1] = dl;
+      P.e[j] = ab;
+      Le2[j] = ab * ab;
+    }
+    P.e[n - 1] = 0;
+    Le2[n - 1] = 0;
+  }
+  for (int j = tid; j < n; j += VBG) P.d[j] = Ld[j];
+  __syncthreads();
+  double* lo = reinterpret_cast<double*>(ws);
+  double* hi = lo + kBigMax;
+  int* cnt = reinterpret_cast<int*>(hi + kBigMax);
+  bisect_all<VBG>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt);
+#ifdef HBM_STAMP
+  __syncthreads();
+  STAMP(6);
+  if (tid == 0 && blockIdx.x == 0)
+    printf("vals_big n=%d stamps: column %llu reflector %llu product %llu dots %llu p/w %llu panel %llu bisect %llu\n", n,
+           stamp_acc[0], stamp_acc[1], stamp_acc[2], stamp_acc[3], stamp_acc[4], stamp_acc[5], stamp_acc[6]);
+#endif
+}
+
 }  // namespace hbm

@@ -78,6 +78,25 @@ def test_c4_w256_step_vs_oracle(c4, warm256):
     eng.close()
 
 
+def test_c4_w256_step_blocked_eigensolver(c4, warm256, monkeypatch):
+    """The same step with every Gram block of order >= 65 on the blocked
+    large-order kernels (k_heev_vals_big + k_heev_bt, config 5's path, which
+    the default routing uses only above order 208): the oracle's bond
+    dimensions and overlaps."""
+    from optimalcontrolmps_amd.native import Engine
+    if "w256/bonds1" not in c4:
+        pytest.skip("w256 oracle fixture not generated")
+    monkeypatch.setenv("OCG_HBM_BIGMIN", "65")
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    psi1 = eng.steps(warm256, np.array([2.5, 3.0]), True)
+    assert list(psi1.bond_dims()) == list(c4["w256/bonds1"])
+    assert abs(eng.overlap(warm256, psi1) - complex(c4["w256/ov01"][0])) <= 1e-10
+    dh = eng.overlap(psi1, psi1, True)
+    assert abs(dh - complex(c4["w256/dH11"][0])) <= 1e-9 * abs(complex(c4["w256/dH11"][0]))
+    assert abs(eng.overlap(psi1, psi1) - 1.0) <= 1e-12
+    eng.close()
+
+
 def test_c4_w256_batched_equals_single(warm256):
     """ocg_step_batch over differently-driven chains == one ocg_step each (bitwise):
     a chain's arithmetic does not depend on what else is in the batch."""

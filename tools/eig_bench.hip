@@ -1,7 +1,7 @@
 // Stand-alone benchmark + residual check of the HBM engine's Hermitian
 // eigensolver kernels on random Gram blocks rho = M M^H (decaying spectrum).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../optimalcontrolmps_amd/csrc tools/eig_bench.hip
-// usage: eig_bench n batch k [regmin]
+// usage: eig_bench n batch k [regmin]   (EIG_OLD=1: orders above RNMAX on the eager L2 kernel)
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <complex>
@@ -79,7 +79,9 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < reps; ++rep) {
     for (int b = 0; b < B; ++b) CK(hipMemcpy(dA + nn * b, As[b].data(), sizeof(z) * nn, hipMemcpyHostToDevice));
     CK(hipEventRecord(e0));
-    {
+    if (n > RNMAX && n <= kBigMax && !getenv("EIG_OLD")) {
+      hipLaunchKernelGGL(k_heev_vals_big, dim3(B), dim3(VBG), 0, 0, dP, didx);
+    } else {
       const int lds = (n >= regmin && n <= RNMAX) ? reg_lds_bytes(reg_grid(n)) : 64 * n + (n <= kLdsOrder ? 16 * n * n : 0) + 64;
       hipLaunchKernelGGL(k_heev_vals_any, dim3(B), dim3(RNT), lds, 0, dP, didx, regmin);
     }
