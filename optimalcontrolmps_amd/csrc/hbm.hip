@@ -17,6 +17,7 @@
 // different block order), Lmat_q' is contiguous, and the right
 // matricisation's column segments are those blocks.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <array>
@@ -503,10 +504,10 @@ struct Engine {
     const GTask* dt_ = upload(t);
     const GSeg* ds = upload(segs);
     hipEvent_t a = get_event(), b = get_event();
-    HCK(hipEventRecord(a, st));
-    hipLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, dt_, int(t.size()), ds);
+    // start / stop events of the dispatch itself (not stream markers around it: with the
+    // host building the next launch's tasks the stream idles between a marker and the kernel)
+    hipExtLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, int(t.size()), ds);
     HCK(hipGetLastError());
-    HCK(hipEventRecord(b, st));
     gemm_ev.push_back({a, b});
     ++gemm_launches;
   }

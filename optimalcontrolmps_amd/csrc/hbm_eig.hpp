@@ -759,7 +759,12 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
     }
   }
   STAMP(1);
-  if (!fast && n <= kBtRows) return;  // U = Q D Z by k_heev_bt
+  if (!fast && n <= kBtRows) {  // U = Q D Z by k_heev_bt
+#ifdef HBM_STAMP
+    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu\n", n, k, stamp_acc[0], stamp_acc[1]);
+#endif
+    return;
+  }
   if (!fast) {
     // U = Q D Z in global memory, reflectors j = n-2 .. 0 (one column per thread)
     z* U = P.U;
