@@ -501,12 +501,18 @@ struct Engine {
       }
       gs_tiles_hist[b] += tiles;
     }
+    std::vector<int> tmap(static_cast<size_t>(tiles));
+    for (size_t i = 0; i < t.size(); ++i) {
+      const int e = i + 1 < t.size() ? t[i + 1].tile0 : tiles;
+      std::fill(tmap.begin() + t[i].tile0, tmap.begin() + e, int(i));
+    }
     const GTask* dt_ = upload(t);
+    const int* dmap = upload(tmap);
     const GSeg* ds = upload(segs);
     hipEvent_t a = get_event(), b = get_event();
     // start / stop events of the dispatch itself (not stream markers around it: with the
     // host building the next launch's tasks the stream idles between a marker and the kernel)
-    hipExtLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, int(t.size()), ds);
+    hipExtLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, dmap, ds);
     HCK(hipGetLastError());
     gemm_ev.push_back({a, b});
     ++gemm_launches;

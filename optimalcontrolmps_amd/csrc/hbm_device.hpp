@@ -115,13 +115,14 @@ __device__ __forceinline__ int find_task(const T* tasks, int ntask, long long e,
 // B[k = l >> 4][l & 15]; results col = l & 15, row = (l >> 4) + 4 r).
 // (GK 32 and 64 measured slower on the config-4 mix: fewer workgroups per CU.)
 constexpr int GT = 32, GK = 16;
-__global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, int ntask,
+__global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, const int* __restrict__ tile_task,
                                              const GSeg* __restrict__ segs) {
   constexpr int EA = GT * GK / NT;  // staged elements per thread and operand
   __shared__ double Ar[GT][GK + 1], Ai[GT][GK + 1], Br[GK][GT + 1], Bi[GK][GT + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int ti = find_task(tasks, ntask, (long long)blockIdx.x, [](const GTask& t) { return (long long)t.tile0; });
-  const GTask T = tasks[ti];
+  // tile -> task from the host's table: one dependent load instead of a binary
+  // search over freshly uploaded task records (the small launches' latency)
+  const GTask T = tasks[tile_task[blockIdx.x]];
   const int tl = blockIdx.x - T.tile0;
   const int ntn = (T.n + GT - 1) / GT;
   const int m0 = (tl / ntn) * GT, n0 = (tl % ntn) * GT;
