@@ -721,6 +721,123 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
       __syncthreads();
     }
   }
+  if (need_gs && !fast && k <= 128 && n <= kBtRows) {
+    // CholeskyQR2 with Z (ld n) in global memory: G (ld k + 1) fills the LDS region,
+    // rows of Z are staged behind it RB at a time; the same formulas and summation
+    // orders as the fast path, the row solve blocked by 16 columns in registers
+    need_gs = false;
+    const int ldg = k + 1;
+    double* G = (double*)un;
+    double* Zs = G + (size_t)k * ldg;
+    const int room = int((size_t(kVecLds) / 8 - (size_t)k * ldg) / size_t(k));
+    const int RB = room < 16 ? room : 16;
+    const int nb8 = (k + 7) >> 3, ntask = k * nb8;
+    constexpr int TPT = (128 * 16 + VNT - 1) / VNT;  // tasks per thread at k = 128
+    for (int pass = 0; pass < 2 && !need_gs; ++pass) {
+      double acc[TPT][8];
+#pragma unroll
+      for (int q = 0; q < TPT; ++q)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[q][t] = 0.0;
+      for (int r0 = 0; r0 < n; r0 += RB) {
+        const int nr = n - r0 < RB ? n - r0 : RB;
+        __syncthreads();
+        for (int e = tid; e < nr * k; e += VNT) {
+          const int rr = e / k, c = e - rr * k;
+          Zs[rr * k + c] = Z[(size_t)(r0 + rr) * n + c];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < TPT; ++q) {
+          const int task = tid + q * VNT;
+          const int i = task / nb8, jb = task - i * nb8;
+          if (task >= ntask || 8 * jb > i) continue;
+          for (int rr = 0; rr < nr; ++rr) {
+            const double* zr = Zs + rr * k;
+            const double zi = zr[i];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[q][t] = fma(zi, zr[8 * jb + t < k ? 8 * jb + t : 0], acc[q][t]);
+          }
+        }
+      }
+      __syncthreads();  // staging done: G may overwrite nothing it still needs (disjoint), order the writes
+#pragma unroll
+      for (int q = 0; q < TPT; ++q) {
+        const int task = tid + q * VNT;
+        const int i = task / nb8, jb = task - i * nb8;
+        if (task >= ntask || 8 * jb > i) continue;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if (8 * jb + t <= i) G[i * ldg + 8 * jb + t] = acc[q][t];
+      }
+      if (tid == 0) chol_fail = 0;
+      __syncthreads();
+      if (wv == 0) {
+        // right-looking Cholesky, lane owns rows lane and lane + 64
+        for (int cc = 0; cc < k; ++cc) {
+          const double dgg = G[cc * ldg + cc];
+          if (!(dgg > 1e-10)) {
+            if (lane == 0) chol_fail = 1;
+            break;
+          }
+          const double dd = sqrt(dgg);
+          double lic[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = lane + 64 * h;
+            lic[h] = (row > cc && row < k) ? G[row * ldg + cc] / dd : 0.0;
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (lane == cc % 64 && cc / 64 == 0) G[cc * ldg + cc] = dd;
+          if (lane == cc % 64 && cc / 64 == 1) G[cc * ldg + cc] = dd;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = lane + 64 * h;
+            if (row > cc && row < k) G[row * ldg + cc] = lic[h];
+          }
+          __builtin_amdgcn_wave_barrier();
+          for (int jj = cc + 1; jj < k; ++jj) {
+            const double ljc = G[jj * ldg + cc];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int row = lane + 64 * h;
+              if (jj <= row && row < k) G[row * ldg + jj] = fma(-lic[h], ljc, G[row * ldg + jj]);
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      __syncthreads();
+      if (chol_fail) { need_gs = true; break; }
+      // Z[r][:] <- Z[r][:] L^-T, one row per thread, 16 columns at a time in registers
+      for (int rr = tid; rr < n; rr += VNT) {
+        double* zr = Z + (size_t)rr * n;
+        for (int b0 = 0; b0 < k; b0 += 16) {
+          double x[16];
+#pragma unroll
+          for (int t = 0; t < 16; ++t) x[t] = b0 + t < k ? zr[b0 + t] : 0.0;
+          for (int i = 0; i < b0; ++i) {
+            const double zi = zr[i];
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+              if (b0 + t < k) x[t] = fma(-zi, G[(b0 + t) * ldg + i], x[t]);
+          }
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {
+            if (b0 + t < k) {
+#pragma unroll
+              for (int s2 = 0; s2 < t; ++s2) x[t] = fma(-x[s2], G[(b0 + t) * ldg + b0 + s2], x[t]);
+              x[t] = x[t] / G[(b0 + t) * ldg + b0 + t];
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < 16; ++t)
+            if (b0 + t < k) zr[b0 + t] = x[t];
+        }
+      }
+      __syncthreads();
+    }
+  }
   if (need_gs) {
     // classical Gram-Schmidt, twice, descending; dots split over 8 row chunks
     for (int j = 0; j < k; ++j) {
