@@ -196,6 +196,9 @@ struct Engine {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gemm_ev;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_kept = nullptr;
+  // side stream: the blocked large-order eigenvalue kernel runs beside the other blocks' kernel
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // smallest Gram order on the register eigensolver (OCG_HBM_REGMIN overrides: A/B and tests)
   int reg_min = kRegMin;
   // smallest Gram order on the blocked kernel k_heev_vals_big (default: the orders the register
@@ -227,6 +230,9 @@ struct Engine {
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& e : gemm_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     if (ev_kept) (void)hipEventDestroy(ev_kept);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (st2) (void)hipStreamDestroy(st2);
     if (st) (void)hipStreamDestroy(st);
   }
 
@@ -239,6 +245,9 @@ struct Engine {
     thost.pinned = true;
     HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
+    HCK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+    HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     md = md_in;
     mdz = mdz_in;
     gate_i1 = gates;
@@ -708,9 +717,13 @@ struct Engine {
       for (int i = 0; i < np; ++i) (R.probs[i].n >= std::max(big_min, 2) && R.probs[i].n <= kBigMax ? big : order).push_back(i);
       std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
       std::stable_sort(big.begin(), big.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
-      if (!big.empty()) {
-        hipLaunchKernelGGL(k_heev_vals_big, dim3(int(big.size())), dim3(VBG), 0, st, R.d_probs, upload(big));
+      if (!big.empty()) {  // on the side stream, after everything st has queued (incl. this upload)
+        const int* dbig = upload(big);
+        HCK(hipEventRecord(ev_fork, st));
+        HCK(hipStreamWaitEvent(st2, ev_fork, 0));
+        hipLaunchKernelGGL(k_heev_vals_big, dim3(int(big.size())), dim3(VBG), 0, st2, R.d_probs, dbig);
         HCK(hipGetLastError());
+        HCK(hipEventRecord(ev_join, st2));
       }
       int lds_v = 64;
       for (int i : order) {
@@ -723,6 +736,7 @@ struct Engine {
                            reg_min);
         HCK(hipGetLastError());
       }
+      if (!big.empty()) HCK(hipStreamWaitEvent(st, ev_join, 0));  // join before the truncation
     }
     int maxnp = 0;
     for (auto& I : items) maxnp = std::max(maxnp, I.np);
