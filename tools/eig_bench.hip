@@ -1,7 +1,7 @@
 // Stand-alone benchmark + residual check of the HBM engine's Hermitian
 // eigensolver kernels on random Gram blocks rho = M M^H (decaying spectrum).
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../optimalcontrolmps_amd/csrc tools/eig_bench.hip
-// usage: eig_bench n batch k [regmin]   (EIG_OLD=1: orders above RNMAX on the eager L2 kernel)
+// usage: eig_bench n batch k [regmin] [thr_rel] [rank]   (EIG_OLD=1: orders above RNMAX on the eager L2 kernel)
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <complex>
@@ -20,6 +20,7 @@ int main(int argc, char** argv) {
   const int kk = std::min(argc > 3 ? atoi(argv[3]) : 32, argc > 1 ? atoi(argv[1]) : 128);
   const int regmin = argc > 4 ? atoi(argv[4]) : kRegMin;
   const double thr_rel = argc > 5 ? atof(argv[5]) : 0.0;
+  const int rank = argc > 6 ? atoi(argv[6]) : n;  // rank of M (rank-deficient Gram blocks: reduced columns, tau = 0)
   const int reps = 5;
   std::mt19937_64 g(7);
   std::normal_distribution<double> N01;
@@ -27,7 +28,7 @@ int main(int argc, char** argv) {
   for (int b = 0; b < B; ++b) {
     std::vector<cd> M(size_t(n) * n), A(size_t(n) * n);
     for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) M[i * n + j] = cd(N01(g), N01(g)) * std::exp(-0.08 * j);
+      for (int j = 0; j < n; ++j) M[i * n + j] = j < rank ? cd(N01(g), N01(g)) * std::exp(-0.08 * j) : cd(0, 0);
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) {
         cd s = 0;

@@ -1,4 +1,4 @@
-# phase stamps of the large-order eigenvalue kernel, then the timing sweep
+# phase stamps of the eigensolver kernels (HBM_STAMP build of tools/eig_bench)
 set -o pipefail
 mkdir -p gpurun_out
-( timeout -k 5 120 ./tools/build/eig_bench_st 448 1 64 ) > gpurun_out/eig_st.log 2>&1 && bash tools/gpu_eigsweep.sh; echo rc=$?
+( for a in "192 1 64" "128 1 32" "448 1 64"; do timeout -k 5 120 ./tools/build/eig_bench_st $a || exit 1; done ) > gpurun_out/eig_st.log 2>&1; echo rc=$?
