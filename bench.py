@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--controls", type=int, default=1,
                     help="K control vectors per GPU evaluated concurrently (K contexts, one host thread and "
                          "stream each: IPOPT trial points / multi-start); value = rows of all K per second")
+    ap.add_argument("--multi", type=int, default=1,
+                    help="K control vectors per GPU in one ocg_hessian_multi call (one pipeline launch for all K); "
+                         "value = rows of all K per second")
     ap.add_argument("--profile-tag", default="r02")
     args = ap.parse_args()
     if args.workload in ("c4grad", "c4rows", "c5rows"):
@@ -105,6 +108,9 @@ def main():
 
     eng = Engine(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"], device=local)
     eng.set_states(tgt, ini)
+    KM = max(1, args.multi)
+    U_multi = np.stack([u] + [np.random.default_rng(CFG["seed"] + 1000 * k + rank).uniform(2.0, 10.0, Nt)
+                              for k in range(1, KM)])
     K = max(1, args.controls)
     extra = []  # controls 2..K of this GPU: own context + stream, own control vector
     for k in range(1, K):
@@ -126,7 +132,11 @@ def main():
         # pipelined launch (rows start as their psi_i appears), then divT, F
         # and the batched <xiH_j|psiH> overlaps (ocg_hessian)
         futs = [pool.submit(e2.hessian, u2, rows) for e2, u2 in extra] if extra else []
-        H, divT, F = eng.hessian(u, rows)
+        if KM > 1:   # all KM controls in one pipeline launch (ocg_hessian_multi)
+            Hm, dm, Fm = eng.hessian_multi(U_multi, rows)
+            H, divT, F = Hm[0], dm[0], Fm[0]
+        else:
+            H, divT, F = eng.hessian(u, rows)
         for f in futs:
             f.result()
         g = dt * (divT * F * 1j).real            # calcFidelityGrad (gamma = 0)
@@ -154,6 +164,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    K = K * KM   # control vectors per GPU per step (contexts x controls per launch)
     rows_total = (Nt - 2) * args.steps * (1 if strong else world) * K
     value = rows_total / elapsed
     st_rows = eng.stats(5)       # k_pipeline: trajectories + row re-propagation (dominant)
@@ -184,7 +195,8 @@ def main():
             "data": "synthetic GRAPE controls U(2,10) seed 20261015; ED ground states U=2.5 -> 50",
             "config": {"workload": "getHessian(u, new_control=true), config 1 (L=5 Npart=5 d=4 maxBondDim=80 "
                                    "tstep=0.01 T=2.0 GRAPE, N_t=201, 199 rows)"
-                                   + (f", {K} concurrent control vectors per GPU" if K > 1 else ""),
+                                   + (f", {K} concurrent control vectors per GPU"
+                                      + (f" ({KM} per pipeline launch)" if KM > 1 else "") if K > 1 else ""),
                        "rows_per_step": (Nt - 2) * (1 if strong else world) * K,
                        "parallelism": (f"one control, rows sharded zig-zag over {world} GPU(s) + RCCL reduce" if strong
                                        else f"{world} GPU(s), one full getHessian (own control vector) per GPU")},

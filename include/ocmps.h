@@ -146,6 +146,17 @@ int ocg_hessian_rows(ocg_ctx* ctx, const double* u, int N, const int* rows, int 
  * device state as ocg_propagate(..,3) + ocg_xi_dH. */
 int ocg_hessian(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                 double* F);
+/* K control vectors u[k*N .. k*N+N) in one call (IPOPT line-search trial
+ * points, finite-difference probes, multi-start; no reference counterpart: the
+ * reference evaluates one getHessian at a time, src/OptimalControl.cpp:281-338).
+ * LDS engine: one k_pipeline launch carries all K controls' psi / xi chains,
+ * xiH workers and rows (tickets keep every waiter behind its producers), then
+ * one batched divT / F launch and one row-overlap launch; per control exactly
+ * the arithmetic of ocg_hessian (the same H bit for bit).  HBM engine: the
+ * controls in turn.  H: K row-major N x N blocks, caller-zeroed; divT: K x 2N;
+ * F: K x 2.  Leaves control 0's trajectories as ocg_hessian would. */
+int ocg_hessian_multi(ocg_ctx* ctx, int K, const double* u, int N, const int* rows, int nrows, double* H,
+                      double* divT, double* F);
 /* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host.
  * Gauge: the chains skip doStep's closing position(1) (src/BH_tDMRG.cpp:206-218)
  * on every step but their last, so an intermediate psi_t / xi_t is the same

@@ -194,18 +194,32 @@ __device__ OCG_INLINE bool await_flag(Chain<NT>& c, const int* flag, int epoch, 
   return ok != 0;
 }
 
+// K control vectors in one launch (ocg_hessian_multi): control k's trajectory
+// slots start k * cs after control 0's, its flags k * (2N + 2) after, its u
+// k * N after; the role ticket counter follows the K flag blocks.  Tickets:
+// [0, 2K) the K psi / xi chain pairs, [2K, 2K + K nxw) the xiH workers, then
+// the rows of all controls interleaved (row r of control k: 2K + K nxw + r K
+// + k), so every waiter still waits only on lower tickets.
 template <int NT>
 __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
-                                         Pool pool, int slot_init, int slot_target, int psi_base, int xi_base,
-                                         int xih_base, const double* u, int N, const int* rows, int nrows,
-                                         const int* rbase, Pool rs, double* rnorm, int* flags, int epoch, int* err,
-                                         int nxw, double* stats) {
+                                         Pool pool, int slot_init, int slot_target, int psi_base0, int xi_base0,
+                                         int xih_base0, const double* u0, int N, const int* rows, int nrows,
+                                         const int* rbase, Pool rs, double* rnorm0, int* flags0, int epoch, int* err,
+                                         int nxw, double* stats, int K, int cs) {
   Chain<NT> c(P, smem);
   if (threadIdx.x == 0)
-    c.ISCAL[14] = __hip_atomic_fetch_add(flags + 2 * N + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c.ISCAL[14] = __hip_atomic_fetch_add(flags0 + K * (2 * N + 2), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const int b = c.ISCAL[14];  // this workgroup's role
+  const int tk = c.ISCAL[14];  // this workgroup's ticket
   __syncthreads();
+  // ticket -> (control kc, role b of the single-control numbering)
+  int kc, b;
+  if (tk < 2 * K) { kc = tk >> 1; b = tk & 1; }
+  else if (tk < 2 * K + K * nxw) { kc = (tk - 2 * K) / nxw; b = 2 + (tk - 2 * K) % nxw; }
+  else { const int t = tk - 2 * K - K * nxw; kc = t % K; b = 2 + nxw + t / K; }
+  const int psi_base = psi_base0 + kc * cs, xi_base = xi_base0 + kc * cs, xih_base = xih_base0 + kc * cs;
+  const double* u = u0 + (size_t)kc * N;
+  int* const flags = flags0 + (size_t)kc * (2 * N + 2);
   c.load_tables(gf, gb, md);
   int* const progress = flags + 2 * N;
   double bytes = 0, flops = 0, nsteps = 0;
@@ -246,8 +260,8 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     c.load(SLOT_D(pool, P, psi_base + i), SLOT_X(pool, P, psi_base + i));
     c.apply_dH();
     const double n2 = c.site_norm2(1);
-    if (threadIdx.x == 0) rnorm[r] = sqrt(n2);
-    int k = rbase[r];
+    if (threadIdx.x == 0) rnorm0[(size_t)kc * nrows + r] = sqrt(n2);
+    int k = kc * rbase[nrows] + rbase[r];  // control kc's row states follow control kc-1's
     c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
     for (int j = i + 1; j + 1 < N; ++j) {  // timeStepper.step(psiH, u[j-1], u[j]) (:269)
       c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
@@ -261,11 +275,14 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
 }
 
 // H_ij from the stored psiH_i(j) (calcHessianRow's two terms, :259-277)
+// K controls (ocg_hessian_multi): pair g of control k = g / total; control
+// k's xiH slots k * cs after control 0's, its divT k * N after, its F at Fp[k],
+// its row norms k * nrows after, its Hessian k * N^2 after.
 template <int NT>
 __device__ OCG_INLINE void body_row_overlaps(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
-                                             Pool pool, int xih_base, const int* rows, int nrows, const int* rbase,
-                                             Pool rs, const double* rnorm, const zc* divT, const zc* Fp, int N,
-                                             double* H, double* stats) {
+                                             Pool pool, int xih_base0, const int* rows, int nrows, const int* rbase,
+                                             Pool rs, const double* rnorm0, const zc* divT0, const zc* Fp, int N,
+                                             double* H0, double* stats, int K, int cs) {
   Chain<NT, true> c(P, smem);
   c.load_tables(gf, gb, md);
   // grid-stride over the (row, column) pairs: a few thousand resident
@@ -273,20 +290,24 @@ __device__ OCG_INLINE void body_row_overlaps(char* smem, OcgParams P, const zc* 
   // the dispatch rate, not by the work)
   const int total = rbase[nrows];
   double b = 0;
-  for (int g = blockIdx.x; g < total; g += gridDim.x) {
-    int lo = 0, hi = nrows - 1;  // row r with rbase[r] <= g < rbase[r+1]
+  for (int g = blockIdx.x; g < K * total; g += gridDim.x) {
+    const int kc = g / total, gl = g - kc * total;
+    int lo = 0, hi = nrows - 1;  // row r with rbase[r] <= gl < rbase[r+1]
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (rbase[mid] <= g) lo = mid;
+      if (rbase[mid] <= gl) lo = mid;
       else hi = mid - 1;
     }
-    const int r = lo, i = rows[r], j = i + (g - rbase[r]);
+    const int r = lo, i = rows[r], j = i + (gl - rbase[r]);
+    const int xih_base = xih_base0 + kc * cs;
     c.load(SLOT_D(rs, P, g), SLOT_X(rs, P, g));
     const zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
     b += 32.0 * c.mps_used();
     if (threadIdx.x == 0) {
-      const zc F = *Fp, di = divT[i], dj = divT[j];
-      const double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? rnorm[r] : 1.0);  // Re(F <xiH_j|psiH> normiH)
+      const zc* divT = divT0 + (size_t)kc * N;
+      double* H = H0 + (size_t)kc * N * N;
+      const zc F = Fp[kc], di = divT[i], dj = divT[j];
+      const double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? rnorm0[(size_t)kc * nrows + r] : 1.0);  // Re(F <xiH_j|psiH> normiH)
       const double v2 = -(di.x * dj.x + di.y * dj.y);                          // -Re(divT_i conj(divT_j))
       const double res = P.dt * P.dt * (v1 + v2);
       H[(size_t)i * N + j] = res;

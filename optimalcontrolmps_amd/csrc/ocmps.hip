@@ -72,19 +72,20 @@ __global__ __launch_bounds__(NT) void k_pipeline(OcgParams P, const zc* gf, cons
                                                  int slot_init, int slot_target, int psi_base, int xi_base,
                                                  int xih_base, const double* u, int N, const int* rows, int nrows,
                                                  const int* rbase, Pool rs, double* rnorm, int* flags, int epoch,
-                                                 int* err, int nxw, double* stats) {
+                                                 int* err, int nxw, double* stats, int K, int cs) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_pipeline<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, xih_base, u, N, rows,
-                         nrows, rbase, rs, rnorm, flags, epoch, err, nxw, stats);
+                         nrows, rbase, rs, rnorm, flags, epoch, err, nxw, stats, K, cs);
 }
 
 __global__ __launch_bounds__(NT) void k_row_overlaps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                      Pool pool, int xih_base, const int* rows, int nrows,
                                                      const int* rbase, Pool rs, const double* rnorm,
-                                                     const zc* divT, const zc* F, int N, double* H, double* stats) {
+                                                     const zc* divT, const zc* F, int N, double* H, double* stats,
+                                                     int K, int cs) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_row_overlaps<NT>(smem, P, gf, gb, md, pool, xih_base, rows, nrows, rbase, rs, rnorm, divT, F, N, H,
-                             stats);
+                             stats, K, cs);
 }
 
 // the same body on one wave per overlap: the contraction's barriers become
@@ -92,10 +93,11 @@ __global__ __launch_bounds__(NT) void k_row_overlaps(OcgParams P, const zc* gf, 
 __global__ __launch_bounds__(64) void k_row_overlaps_w(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                        Pool pool, int xih_base, const int* rows, int nrows,
                                                        const int* rbase, Pool rs, const double* rnorm,
-                                                       const zc* divT, const zc* F, int N, double* H, double* stats) {
+                                                       const zc* divT, const zc* F, int N, double* H, double* stats,
+                                                       int K, int cs) {
   extern __shared__ __align__(16) char smem[];
   ocg::body_row_overlaps<64>(smem, P, gf, gb, md, pool, xih_base, rows, nrows, rbase, rs, rnorm, divT, F, N, H,
-                             stats);
+                             stats, K, cs);
 }
 
 __global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const zc* gb, const int* md,
@@ -1051,6 +1053,9 @@ static int hessian_unfused(ocg_ctx* c, const double* u, int N, const int* rows, 
   return ocg_hessian_rows(c, u, N, rows, nrows, F, divT, H);
 }
 
+static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* rows, int nrows, double* H,
+                         double* divT, double* F);
+
 int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                 double* F) {
   if (!c || !u || !H || !divT || !F || (nrows > 0 && !rows) || nrows < 0 || N < 4)
@@ -1076,6 +1081,15 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     }
     return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
   }
+  return hessian_fused(c, 1, u, N, rows, nrows, H, divT, F);
+}
+
+// The fused LDS-engine getHessian for K control vectors in one k_pipeline launch
+// (K = 1: ocg_hessian).  Control k's trajectories use the slots k * cs after
+// control 0's (cs = 4N), its flags the k-th block of 2N + 2, its row states
+// the k-th block of total; the context keeps control 0's trajectories.
+static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* rows, int nrows, double* H,
+                         double* divT, double* F) {
   if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
   for (int r = 0; r < nrows; ++r)
     if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
@@ -1085,16 +1099,18 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     c->N = N;
     c->have_psi = c->have_xi = c->have_xih = false;
   }
-  if (int rc = ensure_slots(c, 6 + 4 * N)) return rc;
-  if (int rc = ensure_buf(c, c->d_u, c->u_cap, N)) return rc;
-  if (int rc = ensure_buf(c, c->d_pc, c->pc_cap, N + 1)) return rc;
+  const int cs = 4 * N;  // slot stride between controls
+  if (int rc = ensure_slots(c, 6 + cs * K)) return rc;
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, K * N)) return rc;
+  if (int rc = ensure_buf(c, c->d_pc, c->pc_cap, K * (N + 1))) return rc;
   if (int rc = ensure_buf(c, c->d_rows, c->rows_cap, 2 * nrows + 2)) return rc;
-  if (int rc = ensure_buf(c, c->d_prn, c->prn_cap, nrows + 1)) return rc;
-  if (2 * N + 2 > c->flags_cap) {  // publication flags (+ progress counter) start at 0 (< any epoch)
+  if (int rc = ensure_buf(c, c->d_prn, c->prn_cap, K * nrows + 1)) return rc;
+  const int nflags = K * (2 * N + 2) + 1;  // K blocks (psi / xi flags, progress, spare) + the ticket counter
+  if (nflags > c->flags_cap) {  // publication flags (+ progress counter) start at 0 (< any epoch)
     if (c->d_flags) (void)hipFree(c->d_flags);
     c->d_flags = nullptr;
     c->flags_cap = 0;
-    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, 2 * N + 2)) return rc;
+    if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, nflags)) return rc;
     HIPCHK(c, hipMemsetAsync(c->d_flags, 0, sizeof(int) * c->flags_cap, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->epoch = 0;
@@ -1109,9 +1125,16 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
       const char* e = std::getenv("OCG_RS_BUDGET_MB");
       return e ? std::atof(e) : 16384.0;
     }();
-    const double need = double(total) * (sizeof(zc) * double(P.cap) + sizeof(int) * double(P.nsq));
-    if (total > size_t(INT32_MAX / 2) || need > budget_mb * 1048576.0)
-      return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
+    const double need = double(K) * double(total) * (sizeof(zc) * double(P.cap) + sizeof(int) * double(P.nsq));
+    if (size_t(K) * total > size_t(INT32_MAX / 2) || need > budget_mb * 1048576.0) {
+      for (int k = 0; k < K; ++k) {  // controls one after another (last first: control 0's trajectories stay)
+        const int kk = K - 1 - k;
+        if (int rc = hessian_unfused(c, u + size_t(kk) * N, N, rows, nrows, H + size_t(kk) * N * N,
+                                     divT + size_t(kk) * 2 * N, F + 2 * kk))
+          return rc;
+      }
+      return 0;
+    }
   }
   std::vector<int> rb(2 * nrows + 1);  // rows[0..nrows) then rbase[0..nrows]
   total = 0;
@@ -1121,35 +1144,41 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     total += size_t(N - 1 - rows[r]);
   }
   rb[2 * nrows] = int(total);
-  if (total > c->rs_cap) {
+  if (size_t(K) * total > c->rs_cap) {
     if (c->rs.dims) (void)hipFree(c->rs.dims);
     if (c->rs.data) (void)hipFree(c->rs.data);
     c->rs = Pool{nullptr, nullptr};
     c->rs_cap = 0;
-    HIPCHK(c, hipMalloc(&c->rs.dims, sizeof(int) * total * P.nsq));
-    HIPCHK(c, hipMalloc(&c->rs.data, sizeof(zc) * total * P.cap));
-    c->rs_cap = total;
+    HIPCHK(c, hipMalloc(&c->rs.dims, sizeof(int) * K * total * P.nsq));
+    HIPCHK(c, hipMalloc(&c->rs.data, sizeof(zc) * K * total * P.cap));
+    c->rs_cap = size_t(K) * total;
   }
-  size_t hn = size_t(N) * N;
+  size_t hn = size_t(K) * N * N;
   if (hn > c->H_cap) {
     if (c->d_H) (void)hipFree(c->d_H);
     HIPCHK(c, hipMalloc(&c->d_H, sizeof(double) * hn));
     c->H_cap = hn;
   }
   const int epoch = ++c->epoch;
-  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * K * N, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_rows, rb.data(), sizeof(int) * rb.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_flags + 2 * N + 1, 0, sizeof(int), c->stream));  // role tickets
+  HIPCHK(c, hipMemsetAsync(c->d_flags + K * (2 * N + 2), 0, sizeof(int), c->stream));  // role tickets
   const int* d_rows = c->d_rows;
   const int* d_rbase = c->d_rows + nrows;
   // divT_i = <xi_i|dH|psi_i> and F = <psi_{N-1}|target> pair lists
-  std::vector<int> idx(2 * N + 2);
-  for (int i = 0; i < N; ++i) { idx[i] = c->xi_base() + i; idx[N + i] = c->psi_base() + i; }
-  idx[2 * N] = c->psi_base() + N - 1;
-  idx[2 * N + 1] = c->slot_target();
-  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, 2 * N + 2)) return rc;
+  // K N dH pairs (xs then ys), then K F pairs (xs then ys)
+  std::vector<int> idx(2 * K * N + 2 * K);
+  for (int k = 0; k < K; ++k) {
+    for (int i = 0; i < N; ++i) {
+      idx[k * N + i] = c->xi_base() + k * cs + i;
+      idx[K * N + k * N + i] = c->psi_base() + k * cs + i;
+    }
+    idx[2 * K * N + k] = c->psi_base() + k * cs + N - 1;
+    idx[2 * K * N + K + k] = c->slot_target();
+  }
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, int(idx.size()))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
   // the three launches back to back, one host synchronisation at the end;
   // the phase marks give the per-kernel times (ocg_kernel_stats kinds 5, 1, 6)
@@ -1157,17 +1186,18 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
   // xiH workers: the xi chain publishes one state per step and one dH
   // application costs about one step, so a few workers keep up
   const int nxw = std::min(N, kXiHWorkers);
-  hipLaunchKernelGGL(k_pipeline, dim3(2 + nxw + nrows), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb,
-                     c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->xih_base(),
-                     c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err, nxw,
-                     c->d_stats + 5 * 3);
+  hipLaunchKernelGGL(k_pipeline, dim3(K * (2 + nxw + nrows)), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf,
+                     c->d_gb, c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(),
+                     c->xih_base(), c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err,
+                     nxw, c->d_stats + 5 * 3, K, cs);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->evh[1], c->stream));
   const OcgParams Po = c->Po();
-  hipLaunchKernelGGL(k_overlaps, dim3(N), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md, c->pool,
-                     c->d_idx, c->d_idx + N, N, 1, c->d_pc, c->d_stats + 1 * 3);
-  hipLaunchKernelGGL(k_overlaps, dim3(1), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md, c->pool,
-                     c->d_idx + 2 * N, c->d_idx + 2 * N + 1, 1, 0, c->d_pc + N, c->d_stats + 1 * 3);
+  // divT of every control at d_pc[k N + i], F of control k at d_pc[K N + k]
+  hipLaunchKernelGGL(k_overlaps, dim3(K * N), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md,
+                     c->pool, c->d_idx, c->d_idx + K * N, K * N, 1, c->d_pc, c->d_stats + 1 * 3);
+  hipLaunchKernelGGL(k_overlaps, dim3(K), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md, c->pool,
+                     c->d_idx + 2 * K * N, c->d_idx + 2 * K * N + K, K, 0, c->d_pc + K * N, c->d_stats + 1 * 3);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->evh[2], c->stream));
   static const int rov_w = [] {  // A/B switch: OCG_ROWOV_WAVE=0 -> two-wave row overlaps
@@ -1178,22 +1208,23 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     const char* e = std::getenv("OCG_ROWOV_GRID");
     return e ? std::atoi(e) : 4096;
   }();
-  const int rgrid = (rov_grid > 0 && size_t(rov_grid) < total) ? rov_grid : int(total);
+  const size_t ktotal = size_t(K) * total;
+  const int rgrid = (rov_grid > 0 && size_t(rov_grid) < ktotal) ? rov_grid : int(ktotal);
   if (total > 0 && rov_w)
     hipLaunchKernelGGL(k_row_overlaps_w, dim3(unsigned(rgrid)), dim3(64), Po.lds_bytes, c->stream, Po, c->d_gf,
                        c->d_gb, c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
-                       c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
+                       c->d_pc + K * N, N, c->d_H, c->d_stats + 6 * 3, K, cs);
   else if (total > 0)
     hipLaunchKernelGGL(k_row_overlaps, dim3(unsigned(rgrid)), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf,
                        c->d_gb, c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
-                       c->d_pc + N, N, c->d_H, c->d_stats + 6 * 3);
+                       c->d_pc + K * N, N, c->d_H, c->d_stats + 6 * 3, K, cs);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->evh[3], c->stream));
-  std::vector<zc> pc(N + 1);
+  std::vector<zc> pc(size_t(K) * (N + 1));
   std::vector<double> h(hn);
   int err = 0;
   HIPCHK(c, hipMemcpyAsync(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(pc.data(), c->d_pc, sizeof(zc) * (N + 1), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(pc.data(), c->d_pc, sizeof(zc) * K * (N + 1), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const int kinds[3] = {5, 1, 6};
@@ -1213,18 +1244,41 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
                                  ((err & OCG_ERR_JACOBI) ? "eigensolver did not converge within its sweep cap" : ""));
   }
   c->have_psi = c->have_xi = c->have_xih = true;
-  note_u(c, u, N, 3);
-  for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
-  F[0] = pc[N].x;
-  F[1] = pc[N].y;
-  for (int r = 0; r < nrows; ++r) {
-    const int i = rows[r];
-    for (int j = i; j + 1 < N; ++j) {
-      H[size_t(i) * N + j] = h[size_t(i) * N + j];
-      H[size_t(j) * N + i] = h[size_t(j) * N + i];
+  note_u(c, u, N, 3);  // control 0's trajectories stay in the context
+  for (int k = 0; k < K; ++k) {
+    double* Hk = H + size_t(k) * N * N;
+    const double* hk = h.data() + size_t(k) * N * N;
+    for (int i = 0; i < N; ++i) {
+      divT[2 * (size_t(k) * N + i)] = pc[size_t(k) * N + i].x;
+      divT[2 * (size_t(k) * N + i) + 1] = pc[size_t(k) * N + i].y;
+    }
+    F[2 * k] = pc[size_t(K) * N + k].x;
+    F[2 * k + 1] = pc[size_t(K) * N + k].y;
+    for (int r = 0; r < nrows; ++r) {
+      const int i = rows[r];
+      for (int j = i; j + 1 < N; ++j) {
+        Hk[size_t(i) * N + j] = hk[size_t(i) * N + j];
+        Hk[size_t(j) * N + i] = hk[size_t(j) * N + i];
+      }
     }
   }
   return 0;
+}
+
+int ocg_hessian_multi(ocg_ctx* c, int K, const double* u, int N, const int* rows, int nrows, double* H,
+                      double* divT, double* F) {
+  if (!c || !u || !H || !divT || !F || (nrows > 0 && !rows) || nrows < 0 || N < 4 || K < 1)
+    return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (c->hbm || K == 1) {  // HBM engine: its row batches already fill the device; controls in turn
+    for (int k = K - 1; k >= 0; --k)
+      if (int rc = ocg_hessian(c, u + size_t(k) * N, N, rows, nrows, H + size_t(k) * N * N, divT + size_t(k) * 2 * N,
+                               F + 2 * k))
+        return rc;
+    return 0;
+  }
+  for (int r = 0; r < nrows; ++r)
+    if (rows[r] < 1 || rows[r] > N - 2) return fail(c, OCG_EINVAL, "row index out of [1, N-2]");
+  return hessian_fused(c, K, u, N, rows, nrows, H, divT, F);
 }
 
 int ocg_convert_hessian(ocg_ctx* c, const double* Hu, int N, const double* V, int M, double* Hc) {

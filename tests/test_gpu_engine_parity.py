@@ -315,3 +315,24 @@ def test_long_horizon_rows_exceed_cus(states):
     assert np.array_equal(d1, divT) and F1 == F
     assert np.array_equal(H1, H2)
     assert np.isfinite(H1).all() and np.abs(H1).max() > 0
+
+
+@pytest.mark.parametrize("K,Nt", [(3, 201), (2, 41)])
+def test_hessian_multi_equals_single(states, K, Nt):
+    """ocg_hessian_multi: K control vectors in one pipeline launch give each
+    control's ocg_hessian bit for bit (config 1 at its full horizon, and a short
+    one with a row subset), and leave control 0's trajectories in the context"""
+    L, p, N, J = 5, 5, 5, 1.0
+    U = np.random.default_rng(300 + K).uniform(2, 10, (K, Nt))
+    rows = list(range(1, Nt - 1)) if Nt == 201 else [1, 5, 17, Nt - 2]
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    eng.set_states(tgt, ini)
+    Hm, dm, Fm = eng.hessian_multi(U, rows)
+    fid_m = eng.fidelities()
+    for k in range(K):
+        Hs, ds, Fs = eng.hessian(U[k], rows)
+        assert np.array_equal(Hm[k], Hs), k
+        assert np.array_equal(dm[k], ds) and Fm[k] == Fs, k
+        if k == 0:
+            assert np.array_equal(fid_m, eng.fidelities())
