@@ -137,3 +137,20 @@ def test_c4_w256_gradient_fd(warm256):
         num = (cost(up) - cost(um)) / (2 * eps)
         assert abs(g[i] - num) <= 1e-3 * abs(num) + 1e-12, (i, g[i], num)
     eng.close()
+
+
+def test_c4_s32_hessian_multi(c4):
+    """ocg_hessian_multi on the HBM engine (controls in turn): each control's
+    Hessian equals its own ocg_hessian bit for bit; control 0 = the golden one"""
+    from optimalcontrolmps_amd.native import Engine
+    u0 = c4["s32/u"]
+    Nt = len(u0)
+    U = np.stack([u0, np.random.default_rng(11).uniform(2.0, 10.0, Nt)])
+    eng = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+    eng.set_states(_mps(c4["s32/tgt_dims"], c4["s32/tgt_data"]), _mps(c4["s32/init_dims"], c4["s32/init_data"]))
+    Hm, dm, Fm = eng.hessian_multi(U)
+    assert np.abs(Hm[0] - c4["s32/H"]).max() <= 1e-6 * np.abs(c4["s32/H"]).max()
+    for k in range(2):
+        Hs, ds, Fs = eng.hessian(U[k])
+        assert np.array_equal(Hm[k], Hs) and np.array_equal(dm[k], ds) and Fm[k] == Fs, k
+    eng.close()
