@@ -446,6 +446,24 @@ struct Engine {
     return (const T*)d;
   }
 
+  // three task arrays in one host-to-device copy (each 256-byte aligned)
+  template <class A, class B, class C>
+  void upload3(const std::vector<A>& a, const std::vector<B>& b, const std::vector<C>& c, const A*& da,
+               const B*& db, const C*& dc) {
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t ba = sizeof(A) * a.size(), bb = sizeof(B) * b.size(), bc = sizeof(C) * c.size();
+    const size_t oa = 0, ob = al(ba), oc = ob + al(bb), bytes = std::max<size_t>(oc + bc, 1);
+    char* h = thost.get(bytes);
+    char* d = tdev.get(bytes);
+    if (ba) std::memcpy(h + oa, a.data(), ba);
+    if (bb) std::memcpy(h + ob, b.data(), bb);
+    if (bc) std::memcpy(h + oc, c.data(), bc);
+    HCK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    da = ba ? (const A*)(d + oa) : nullptr;
+    db = bb ? (const B*)(d + ob) : nullptr;
+    dc = bc ? (const C*)(d + oc) : nullptr;
+  }
+
   // ------------------------------------------------------------ launches
   hipEvent_t get_event() {
     if (!ev_pool.empty()) {
@@ -515,9 +533,10 @@ struct Engine {
       const int e = i + 1 < t.size() ? t[i + 1].tile0 : tiles;
       std::fill(tmap.begin() + t[i].tile0, tmap.begin() + e, int(i));
     }
-    const GTask* dt_ = upload(t);
-    const int* dmap = upload(tmap);
-    const GSeg* ds = upload(segs);
+    const GTask* dt_;
+    const int* dmap;
+    const GSeg* ds;
+    upload3(t, tmap, segs, dt_, dmap, ds);
     hipEvent_t a = get_event(), b = get_event();
     // start / stop events of the dispatch itself (not stream markers around it: with the
     // host building the next launch's tasks the stream idles between a marker and the kernel)
