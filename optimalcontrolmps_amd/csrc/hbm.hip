@@ -756,14 +756,6 @@ struct Engine {
         HCK(hipGetLastError());
       }
       if (!big.empty()) HCK(hipStreamWaitEvent(st, ev_join, 0));  // join before the truncation
-      // eigenvalues of the register / blocked reductions' tridiagonals
-      std::vector<int> bis(big);
-      for (int i : order)
-        if (R.probs[i].n >= reg_min && R.probs[i].n <= RNMAX) bis.push_back(i);
-      if (!bis.empty()) {
-        hipLaunchKernelGGL(k_heev_bisect, dim3(int(bis.size())), dim3(RNT), 0, st, R.d_probs, upload(bis));
-        HCK(hipGetLastError());
-      }
     }
     int maxnp = 0;
     for (auto& I : items) maxnp = std::max(maxnp, I.np);

@@ -432,7 +432,14 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
     se2[n - 1] = 0;
   }
   for (int j = tid; j < n; j += RNT) P.d[j] = sd[j];
-  // the eigenvalues: k_heev_bisect, at full occupancy, once this CU is free
+  __syncthreads();
+  // ---- eigenvalues (work arrays reuse the partial buffers)
+  double* lo = (double*)&rowbuf[0][0][0];
+  double* hi = lo + NM;
+  int* cnt = (int*)(hi + NM);
+#ifndef HBM_NO_BISECT  // timing builds of tools/eig_bench only
+  bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt);
+#endif
 }
 
 // One launch per decomposition: each workgroup picks the variant for its
@@ -1335,7 +1342,11 @@ __global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__
     Le2[n - 1] = 0;
   }
   for (int j = tid; j < n; j += VBG) P.d[j] = Ld[j];
-  // the eigenvalues: k_heev_bisect
+  __syncthreads();
+  double* lo = reinterpret_cast<double*>(ws);
+  double* hi = lo + kBigMax;
+  int* cnt = reinterpret_cast<int*>(hi + kBigMax);
+  bisect_all<VBG>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt);
 #ifdef HBM_STAMP
   __syncthreads();
   STAMP(6);
@@ -1343,28 +1354,6 @@ __global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__
     printf("vals_big n=%d stamps: column %llu reflector %llu product %llu dots %llu p/w %llu panel %llu bisect %llu\n", n,
            stamp_acc[0], stamp_acc[1], stamp_acc[2], stamp_acc[3], stamp_acc[4], stamp_acc[5], stamp_acc[6]);
 #endif
-}
-
-// ------------------------------------------------------------------ eigenvalues
-// All eigenvalues of the real tridiagonals (P.d, P.e) that the register and
-// blocked reductions leave behind, by the multisection of bisect_all (256
-// threads per problem, the arithmetic the register kernel used inline).  As a
-// kernel of its own it runs at full occupancy (~20 KB of LDS, few registers:
-// several problems per CU) instead of on one wave per SIMD of a CU that the
-// next reduction is waiting for.
-__global__ __launch_bounds__(RNT) void k_heev_bisect(const EProb* __restrict__ probs, const int* __restrict__ idx) {
-  __shared__ double Ld[kBigMax], Le2[kBigMax], lo[kBigMax], hi[kBigMax];
-  __shared__ int cnt[4 * RNT];
-  const EProb P = probs[idx[blockIdx.x]];
-  const int n = P.n;
-  if (n < 2 || n > kBigMax) return;
-  for (int i = threadIdx.x; i < n; i += RNT) {
-    Ld[i] = P.d[i];
-    const double e = P.e[i];
-    Le2[i] = e * e;
-  }
-  __syncthreads();
-  bisect_all<RNT>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt);
 }
 
 }  // namespace hbm

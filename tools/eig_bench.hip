@@ -86,8 +86,6 @@ int main(int argc, char** argv) {
       const int lds = (n >= regmin && n <= RNMAX) ? reg_lds_bytes(reg_grid(n)) : 64 * n + (n <= kLdsOrder ? 16 * n * n : 0) + 64;
       hipLaunchKernelGGL(k_heev_vals_any, dim3(B), dim3(RNT), lds, 0, dP, didx, regmin);
     }
-    if (n >= 2 && ((n >= regmin && n <= RNMAX) || (n > RNMAX && n <= kBigMax && !getenv("EIG_OLD"))))
-      hipLaunchKernelGGL(k_heev_bisect, dim3(B), dim3(RNT), 0, 0, dP, didx);
     CK(hipEventRecord(e1));
     hipLaunchKernelGGL(k_heev_vecs_reg, dim3(B), dim3(VNT), 0, 0, dP, B);
     if (dbt) hipLaunchKernelGGL(k_heev_bt, dim3(int(bt.size())), dim3(BNT), 0, 0, dP, dbt);
