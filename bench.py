@@ -360,6 +360,15 @@ def bench_c4(args):
         eng.xi_dH()
         return eng.hessian_rows(u, rows, F, divT)
 
+    import threading
+    done = threading.Event()
+
+    def heartbeat():   # long slices (full N_t): a line a minute on stderr while the device works
+        t_hb = time.perf_counter()
+        while not done.wait(60.0):
+            print(f"[bench] {args.workload} N_t={Nt}: {time.perf_counter() - t_hb:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     for _ in range(args.warmup):
         one()
     eng.reset_stats()
@@ -369,6 +378,7 @@ def bench_c4(args):
         one()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    done.set()
     gm = eng.stats(7)   # k_gemm: the MFMA-FP64 contraction kernel
     st_traj = eng.stats(0)
     steps_traj = 2 * (Nt - 1)
