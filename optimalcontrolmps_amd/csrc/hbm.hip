@@ -188,6 +188,7 @@ struct Engine {
   long gemm_launches = 0;
   // OCG_GEMM_STATS=1: shape statistics of the GEMM launches, printed at destruction (diagnostic)
   bool gstat = std::getenv("OCG_GEMM_STATS") != nullptr;
+  long eig_hist[34] = {0};  // Gram block orders in bins of 16 (OCG_GEMM_STATS)
   double gs_pad = 0, gs_flop = 0, gs_tiles_hist[6] = {0}, gs_flop_m[6] = {0}, gs_flop_k[6] = {0};
   long gs_launch_hist[6] = {0};
   double gs_ms[6] = {0}, gs_bflop[6] = {0}, gs_ntask[6] = {0}, gs_nseg[6] = {0}, gs_m[6] = {0}, gs_n[6] = {0}, gs_k[6] = {0};
@@ -226,6 +227,14 @@ struct Engine {
           std::fprintf(stderr, "[gemm] %-6s tasks/launch %.1f  segs/task %.2f  avg m %.1f n %.1f k/seg %.1f\n", lb[b],
                        gs_ntask[b] / std::max<long>(gs_launch_hist[b], 1), gs_nseg[b] / gs_ntask[b], gs_m[b] / gs_ntask[b],
                        gs_n[b] / gs_ntask[b], gs_k[b] / std::max(gs_nseg[b], 1.0));
+    }
+    if (gstat) {
+      long tot = 0;
+      for (long v : eig_hist) tot += v;
+      std::fprintf(stderr, "[eig] Gram blocks %ld by order:", tot);
+      for (int b = 0; b < 34; ++b)
+        if (eig_hist[b]) std::fprintf(stderr, " %d-%d:%ld", 16 * b, 16 * b + 15, eig_hist[b]);
+      std::fprintf(stderr, "\n");
     }
     for (auto& e : ev_pool) (void)hipEventDestroy(e);
     for (auto& e : gemm_ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -735,6 +744,8 @@ struct Engine {
       std::vector<int> order, big;
       for (int i = 0; i < np; ++i) (R.probs[i].n >= std::max(big_min, 2) && R.probs[i].n <= kBigMax ? big : order).push_back(i);
       std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
+      if (gstat)
+        for (int i = 0; i < np; ++i) ++eig_hist[std::min(R.probs[i].n / 16, 33)];
       std::stable_sort(big.begin(), big.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
       if (!big.empty()) {  // on the side stream, after everything st has queued (incl. this upload)
         const int* dbig = upload(big);
