@@ -168,6 +168,21 @@ struct ocg_ctx {
     q.lds_bytes = lds_ovl;
     return q;
   }
+  // chain parameter block sized for two chain workgroups per CU (plan slots
+  // shrunk to half the LDS, or none): many concurrent chains (ocg_hessian_multi)
+  int plan_pe2 = 0, lds2 = 0;
+  OcgParams P2() const {
+    OcgParams q = P;
+    if (plan_pe2 >= 32) {
+      q.plan_pe = plan_pe2;
+      q.lds_bytes = lds2;
+    } else {
+      q.nplan = 0;
+      q.plan_pe = 0;
+      q.lds_bytes = lds_np;
+    }
+    return q;
+  }
   // parameter block of those kernels: plans off, smaller LDS
   OcgParams Pn() const {
     OcgParams q = P;
@@ -440,7 +455,9 @@ static int finish_params(ocg_ctx* c) {
   // left over (a decomposition larger than its slot just runs unplanned)
   const char* np = std::getenv("OCG_NO_PLANS");  // diagnostic / test switch: general path only
   const bool plans_off = np && np[0] && np[0] != '0';
-  if (!plans_off && c->P.cap < 65536 && c->P.thcap < 65536 && c->P.evcap < 4096) {
+  // plan slot capacity (elements) that fits `lim` bytes of LDS, 0 if none
+  auto plan_fit = [&](size_t lim, int& bytes) {
+    if (plans_off || !(c->P.cap < 65536 && c->P.thcap < 65536 && c->P.evcap < 4096)) return 0;
     OcgParams q = c->P;
     q.nplan = q.ngates + ocg_host::step_gauge_moves(q);
     q.plan_pe = 0;
@@ -448,13 +465,21 @@ static int finish_params(ocg_ctx* c) {
     q.plan_pe = 64;
     const int per = (ocg::lds_layout(q, NT).bytes - b0 + 63) / 64;  // bytes per element, all slots
     const int want = std::max(q.th2cap, q.max_site_cap);
-    q.plan_pe = std::min(want, per > 0 ? int((long(limit) - b0) / per) - 8 : 0);
-    while (q.plan_pe >= 32 && size_t(ocg::lds_layout(q, NT).bytes) > limit) q.plan_pe -= 8;
-    if (q.plan_pe >= 32) {
-      c->P.nplan = q.nplan;
-      c->P.plan_pe = q.plan_pe;
-      c->P.lds_bytes = ocg::lds_layout(q, NT).bytes;
-    }
+    q.plan_pe = std::min(want, per > 0 ? int((long(lim) - b0) / per) - 8 : 0);
+    while (q.plan_pe >= 32 && size_t(ocg::lds_layout(q, NT).bytes) > lim) q.plan_pe -= 8;
+    if (q.plan_pe < 32) return 0;
+    bytes = ocg::lds_layout(q, NT).bytes;
+    return q.plan_pe;
+  };
+  const int nplan = c->P.ngates + ocg_host::step_gauge_moves(c->P);  // slots: one per decomposition of a step
+  int b1 = 0, b2 = 0;
+  const int pe1 = plan_fit(limit, b1);                                            // one chain per CU
+  c->plan_pe2 = plan_fit(std::max<size_t>(size_t(l.bytes), limit / 2), b2);      // two chains per CU
+  c->lds2 = b2;
+  if (pe1 >= 32) {
+    c->P.nplan = nplan;
+    c->P.plan_pe = pe1;
+    c->P.lds_bytes = b1;
   }
   if (size_t(l.bytes) > limit)
     return fail(c, OCG_ECAP,
@@ -1186,7 +1211,14 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   // xiH workers: the xi chain publishes one state per step and one dH
   // application costs about one step, so a few workers keep up
   const int nxw = std::min(N, kXiHWorkers);
-  hipLaunchKernelGGL(k_pipeline, dim3(K * (2 + nxw + nrows)), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf,
+  // many controls: chain workgroups sized for two per CU (smaller plan slots; plans are
+  // bitwise-neutral) — measured 37.3k vs 33.0k rows/s at K = 8, slower below (OCG_MULTI_SHARE_K)
+  static const int share_k = [] {
+    const char* e = std::getenv("OCG_MULTI_SHARE_K");
+    return e ? std::atoi(e) : 8;
+  }();
+  const OcgParams Pl = (share_k > 0 && K >= share_k) ? c->P2() : P;
+  hipLaunchKernelGGL(k_pipeline, dim3(K * (2 + nxw + nrows)), dim3(NT), Pl.lds_bytes, c->stream, Pl, c->d_gf,
                      c->d_gb, c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(),
                      c->xih_base(), c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err,
                      nxw, c->d_stats + 5 * 3, K, cs);

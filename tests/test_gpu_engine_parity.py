@@ -336,3 +336,18 @@ def test_hessian_multi_equals_single(states, K, Nt):
         assert np.array_equal(dm[k], ds) and Fm[k] == Fs, k
         if k == 0:
             assert np.array_equal(fid_m, eng.fidelities())
+
+
+def test_hessian_multi_shared_cu_layout_bitwise(states, monkeypatch):
+    """K >= OCG_MULTI_SHARE_K runs the chains with the two-per-CU LDS layout
+    (smaller plan slots): the same Hessians bit for bit"""
+    monkeypatch.setenv("OCG_MULTI_SHARE_K", "2")
+    L, p, N, J = 5, 5, 5, 1.0
+    U = np.random.default_rng(404).uniform(2, 10, (2, 61))
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    eng.set_states(tgt, ini)
+    Hm, dm, Fm = eng.hessian_multi(U)
+    for k in range(2):
+        Hs, ds, Fs = eng.hessian(U[k])
+        assert np.array_equal(Hm[k], Hs) and np.array_equal(dm[k], ds) and Fm[k] == Fs, k
