@@ -120,7 +120,7 @@ def main():
     Hdev = torch.zeros((Nt, Nt), dtype=torch.float64, device=cdev)
 
     if args.workload == "gradient":
-        return bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev)
+        return bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev, U_multi)
 
     pool = None
     if extra:
@@ -255,14 +255,19 @@ def roofline_block(kernel, launch_ms, bytes_per_launch, flops_per_launch, tag, l
     }
 
 
-def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev):
+def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev, U_multi):
     """config 2: getAnalyticGradient(u) with BFGS=true at config 1 — psi_t and xi_t
     propagated concurrently in one launch (calcFidelityGrad's BFGS branch,
     src/OptimalControl.cpp:217-229, propagates xi independently of psi), then the
     batched divT overlaps and F (ocg_propagate(u, 3) + ocg_div_t + ocg_overlap_factor)."""
     import torch
 
+    KM = len(U_multi)
+
     def one():
+        if KM > 1:   # K control vectors: one trajectory launch of 2K chains + batched divT / F
+            divT, F = eng.gradient_multi(U_multi)
+            return dt * (divT * F[:, None] * 1j).real
         eng.propagate(u, 3)
         divT = eng.div_t()
         F = eng.overlap_factor()
@@ -290,12 +295,13 @@ def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev):
         launch_ms = st_traj["ms"] / max(1, st_traj["launches"])
         res = {
             "metric": "getAnalyticGradient/sec (BFGS=true: psi || xi + divT), N=5 d=4 chi=80 T=2.0",
-            "value": args.steps * world / elapsed, "unit": "gradients/s", "n_gpus": world,
+            "value": args.steps * world * KM / elapsed, "unit": "gradients/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c128/f64",
             "data": "synthetic GRAPE controls U(2,10) seed 20261015; ED ground states U=2.5 -> 50",
-            "config": {"workload": "config 2: getAnalyticGradient(u, new_control=true), BFGS=true, N_t=201"},
-            "sweep_steps_per_sec": args.steps * world * 2 * (Nt - 1) / elapsed,
+            "config": {"workload": "config 2: getAnalyticGradient(u, new_control=true), BFGS=true, N_t=201"
+                                   + (f", {KM} control vectors per call (ocg_gradient_multi)" if KM > 1 else "")},
+            "sweep_steps_per_sec": args.steps * world * KM * 2 * (Nt - 1) / elapsed,
             "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(launch_ms, 1e-9),
             "kernels": {"trajectory_ms": launch_ms, "divT_F_ms": st_ov["ms"] / max(1, args.steps)},
             "roofline": roofline_block("k_trajectory", launch_ms, st_traj["alg_bytes"] / max(1, st_traj["launches"]),

@@ -157,6 +157,14 @@ int ocg_hessian(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows
  * F: K x 2.  Leaves control 0's trajectories as ocg_hessian would. */
 int ocg_hessian_multi(ocg_ctx* ctx, int K, const double* u, int N, const int* rows, int nrows, double* H,
                       double* divT, double* F);
+/* The gradient's device work (calcPsi || calcXi + divT + F, the BFGS path of
+ * calcFidelityGrad, src/OptimalControl.cpp:204-249) for K control vectors
+ * u[k*N .. k*N+N) in one call: LDS engine, one trajectory launch of 2K chains
+ * and one batched divT / F launch each (per control exactly the arithmetic of
+ * ocg_propagate(..,3) + ocg_div_t + ocg_overlap_factor); HBM engine, the
+ * controls in turn.  divT: K x 2N, F: K x 2; grad_k,i = dt Re(i divT_k,i F_k)
+ * (plus the caller's regularisation).  Leaves control 0's trajectories. */
+int ocg_gradient_multi(ocg_ctx* ctx, int K, const double* u, int N, double* divT, double* F);
 /* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host.
  * Gauge: the chains skip doStep's closing position(1) (src/BH_tDMRG.cpp:206-218)
  * on every step but their last, so an intermediate psi_t / xi_t is the same

@@ -42,11 +42,17 @@ struct Pool {
 // --------------------------------------------------------------------------
 template <int NT>
 __device__ OCG_INLINE void body_trajectory(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
-                                                   Pool pool, int slot_init, int slot_target, int psi_base,
-                                                   int xi_base, const double* u, int N, int which, double* stats) {
+                                                   Pool pool, int slot_init, int slot_target, int psi_base0,
+                                                   int xi_base0, const double* u0, int N, int which, double* stats,
+                                                   int cs) {
   Chain<NT> c(P, smem);
   c.load_tables(gf, gb, md);
-  int chain = (which == 3) ? blockIdx.x : (which == 1 ? 0 : 1);
+  // which == 3: workgroup 2k + {0, 1} = control k's psi / xi chain (ocg_gradient_multi:
+  // control k's slots cs after control k-1's, its controls N after)
+  int chain = (which == 3) ? (blockIdx.x & 1) : (which == 1 ? 0 : 1);
+  const int kc = (which == 3) ? (blockIdx.x >> 1) : 0;
+  const int psi_base = psi_base0 + kc * cs, xi_base = xi_base0 + kc * cs;
+  const double* u = u0 + (size_t)kc * N;
   // chain 0: psi_t forward from psi_init (calcPsi, src/OptimalControl.cpp:375-390)
   // chain 1: xi_t backward from psi_target (calcXi, :392-407)
   const int fwd = (chain == 0) ? 1 : 0;

@@ -40,9 +40,11 @@ using ocg::Pool;
 // __global__ entry points
 __global__ __launch_bounds__(NT) void k_trajectory(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                    Pool pool, int slot_init, int slot_target, int psi_base,
-                                                   int xi_base, const double* u, int N, int which, double* stats) {
+                                                   int xi_base, const double* u, int N, int which, double* stats,
+                                                   int cs) {
   extern __shared__ __align__(16) char smem[];
-  ocg::body_trajectory<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, u, N, which, stats);
+  ocg::body_trajectory<NT>(smem, P, gf, gb, md, pool, slot_init, slot_target, psi_base, xi_base, u, N, which, stats,
+                           cs);
 }
 
 __global__ __launch_bounds__(NT) void k_overlaps(OcgParams P, const zc* gf, const zc* gb, const int* md,
@@ -930,11 +932,59 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
   if (int rc = begin_kernel(c)) return rc;
   hipLaunchKernelGGL(k_trajectory, dim3(grid), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
                      c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->d_u, N, which,
-                     c->d_stats + 0 * 3);
+                     c->d_stats + 0 * 3, 0);
   if (int rc = end_kernel(c, 0)) return rc;
   if (which & 1) { c->have_psi = true; c->have_xih = c->have_xih && (which & 2); }
   if (which & 2) { c->have_xi = true; c->have_xih = false; }
   note_u(c, u, N, which);
+  return 0;
+}
+
+int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, double* F) {
+  if (!c || !u || !divT || !F || N < 2 || K < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (c->hbm || K == 1) {  // controls in turn (last first: control 0's trajectories stay)
+    for (int k = K - 1; k >= 0; --k) {
+      if (int rc = ocg_propagate(c, u + size_t(k) * N, N, 3)) return rc;
+      if (int rc = ocg_div_t(c, divT + size_t(k) * 2 * N)) return rc;
+      if (int rc = ocg_overlap_factor(c, F + 2 * k)) return rc;
+    }
+    return 0;
+  }
+  if (!c->have_states) return fail(c, OCG_ESTATE, "ocg_set_states first");
+  HIPCHK(c, hipSetDevice(c->device));
+  const OcgParams& P = c->P;
+  if (N != c->N) {
+    c->N = N;
+    c->have_psi = c->have_xi = c->have_xih = false;
+  }
+  c->u_psi.clear();
+  c->u_xi.clear();
+  const int cs = 4 * N;  // slot stride between controls (as ocg_hessian_multi)
+  if (int rc = ensure_slots(c, 6 + cs * K)) return rc;
+  if (int rc = ensure_buf(c, c->d_u, c->u_cap, K * N)) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * K * N, hipMemcpyHostToDevice, c->stream));
+  if (int rc = begin_kernel(c)) return rc;
+  hipLaunchKernelGGL(k_trajectory, dim3(2 * K), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+                     c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->d_u, N, 3,
+                     c->d_stats + 0 * 3, cs);
+  if (int rc = end_kernel(c, 0)) return rc;
+  c->have_psi = c->have_xi = true;
+  c->have_xih = false;
+  note_u(c, u, N, 3);  // control 0's trajectories stay in the context
+  // divT of every control (<xi_i|dH|psi_i>, ocg_div_t's pairs), then every F (<psi_{N-1}|target>)
+  std::vector<int> xs(size_t(K) * N), ys(size_t(K) * N);
+  for (int k = 0; k < K; ++k)
+    for (int i = 0; i < N; ++i) {
+      xs[size_t(k) * N + i] = c->xi_base() + k * cs + i;
+      ys[size_t(k) * N + i] = c->psi_base() + k * cs + i;
+    }
+  std::vector<zc> r;
+  if (int rc = launch_overlaps(c, xs, ys, 1, r)) return rc;
+  for (size_t e = 0; e < size_t(K) * N; ++e) { divT[2 * e] = r[e].x; divT[2 * e + 1] = r[e].y; }
+  std::vector<int> fx(K), fy(K, c->slot_target());
+  for (int k = 0; k < K; ++k) fx[k] = c->psi_base() + k * cs + N - 1;
+  if (int rc = launch_overlaps(c, fx, fy, 0, r)) return rc;
+  for (int k = 0; k < K; ++k) { F[2 * k] = r[k].x; F[2 * k + 1] = r[k].y; }
   return 0;
 }
 

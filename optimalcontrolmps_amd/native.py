@@ -110,6 +110,7 @@ SIGNATURES = [
     ("ocg_hessian_rows", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_hessian", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_hessian_multi", C.c_int, [C.c_void_p, C.c_int, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
+    ("ocg_gradient_multi", C.c_int, [C.c_void_p, C.c_int, dp, C.c_int, dp, dp]),
     ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_convert_hessian", C.c_int, [C.c_void_p, dp, C.c_int, dp, C.c_int, dp]),
     ("ocg_kernel_stats", C.c_int, [C.c_void_p, C.c_int, dp, C.POINTER(C.c_long), dp, dp, C.POINTER(C.c_long)]),
@@ -351,6 +352,18 @@ class Engine:
         self._chk(lib().ocg_hessian_multi(self.h, K, Um.ctypes.data_as(dp), N, pr, len(r), H.ctypes.data_as(dp),
                                           dv.ctypes.data_as(dp), Fa.ctypes.data_as(dp)), "ocg_hessian_multi")
         return H, dv.view(np.complex128).copy(), Fa[:, 0] + 1j * Fa[:, 1]
+
+    def gradient_multi(self, U):
+        """psi || xi + divT + F for K control vectors (rows of U) in one call:
+        returns (divT (K, N), F (K,)); the device keeps control 0's trajectories"""
+        Um = np.ascontiguousarray(np.atleast_2d(np.asarray(U, dtype=np.float64)))
+        K, N = Um.shape
+        self.N = N
+        dv = np.zeros((K, 2 * N))
+        Fa = np.zeros((K, 2))
+        self._chk(lib().ocg_gradient_multi(self.h, K, Um.ctypes.data_as(dp), N, dv.ctypes.data_as(dp),
+                                           Fa.ctypes.data_as(dp)), "ocg_gradient_multi")
+        return dv.view(np.complex128).copy(), Fa[:, 0] + 1j * Fa[:, 1]
 
     def convert_hessian(self, Hu, V):
         """ControlBasis::convertHessian on the device: V Hu V^T (V is M x N)"""

@@ -351,3 +351,22 @@ def test_hessian_multi_shared_cu_layout_bitwise(states, monkeypatch):
     for k in range(2):
         Hs, ds, Fs = eng.hessian(U[k])
         assert np.array_equal(Hm[k], Hs) and np.array_equal(dm[k], ds) and Fm[k] == Fs, k
+
+
+@pytest.mark.parametrize("K", [1, 5])
+def test_gradient_multi_equals_single(states, K):
+    """ocg_gradient_multi: K controls' psi || xi (one launch of 2K chains) and
+    batched divT / F equal ocg_propagate(.., 3) + ocg_div_t + ocg_overlap_factor
+    per control bit for bit; control 0's trajectories stay"""
+    L, p, N, J = 5, 5, 5, 1.0
+    U = np.random.default_rng(500 + K).uniform(2, 10, (K, 201))
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    eng.set_states(tgt, ini)
+    dm, Fm = eng.gradient_multi(U)
+    fid_m = eng.fidelities()
+    for k in range(K):
+        eng.propagate(U[k], 3)
+        assert np.array_equal(dm[k], eng.div_t()) and Fm[k] == eng.overlap_factor(), k
+        if k == 0:
+            assert np.array_equal(fid_m, eng.fidelities())
