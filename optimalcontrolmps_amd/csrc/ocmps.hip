@@ -942,6 +942,7 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
 
 int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, double* F) {
   if (!c || !u || !divT || !F || N < 2 || K < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (size_t(K) * 4 * size_t(N) + 6 > size_t(INT32_MAX)) return fail(c, OCG_EINVAL, "K * N too large");
   if (c->hbm || K == 1) {  // controls in turn (last first: control 0's trajectories stay)
     for (int k = K - 1; k >= 0; --k) {
       if (int rc = ocg_propagate(c, u + size_t(k) * N, N, 3)) return rc;
@@ -1351,6 +1352,8 @@ int ocg_hessian_multi(ocg_ctx* c, int K, const double* u, int N, const int* rows
                       double* divT, double* F) {
   if (!c || !u || !H || !divT || !F || (nrows > 0 && !rows) || nrows < 0 || N < 4 || K < 1)
     return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (size_t(K) * 4 * size_t(N) + 6 > size_t(INT32_MAX) || size_t(K) * N * N > (size_t(1) << 40))
+    return fail(c, OCG_EINVAL, "K * N too large");
   if (c->hbm || K == 1) {  // HBM engine: its row batches already fill the device; controls in turn
     for (int k = K - 1; k >= 0; --k)
       if (int rc = ocg_hessian(c, u + size_t(k) * N, N, rows, nrows, H + size_t(k) * N * N, divT + size_t(k) * 2 * N,
