@@ -172,6 +172,24 @@ def main():
     t_tr = time.perf_counter()
     eng.propagate(u, 3)          # one bare psi || xi trajectory (outside the timed region): single-chain step rate
     t_tr = time.perf_counter() - t_tr
+    # throughput with several control vectors per call (IPOPT trial points, FD probes,
+    # multi-start), outside the timed region: reported beside `value`, never as it
+    multi_info = None
+    if K * KM == 1 and not strong:
+        Um = np.random.default_rng(CFG["seed"] + 77 + rank).uniform(2.0, 10.0, (8, Nt))
+        eng.hessian_multi(Um[:2], rows)              # warm the multi path's buffers
+        torch.cuda.synchronize()
+        t_m = time.perf_counter()
+        eng.hessian_multi(Um, rows)
+        t_m = time.perf_counter() - t_m
+        Ug = np.random.default_rng(CFG["seed"] + 78 + rank).uniform(2.0, 10.0, (64, Nt))
+        eng.gradient_multi(Ug[:2])
+        t_g = time.perf_counter()
+        eng.gradient_multi(Ug)
+        t_g = time.perf_counter() - t_g
+        multi_info = {"hessian_rows_per_sec_8_controls": 8 * len(rows) / t_m,
+                      "gradients_per_sec_64_controls": 64 / t_g,
+                      "note": "ocg_hessian_multi / ocg_gradient_multi, one launch for all controls, per GPU"}
     row_steps = (Nt - 2) * (Nt - 3) // 2
     sweep_steps = args.steps * K * (2 * (Nt - 1) * world + row_steps * (1 if strong else world))
     result = None
@@ -207,6 +225,7 @@ def main():
                 "divT_F_overlaps_ms": eng.stats(1)["ms"] / max(1, args.steps),
             },
             "single_chain_steps_per_sec": (Nt - 1) / t_tr,
+            "multi_control": multi_info,
             "roofline": roofline_block("k_pipeline", launch_ms, bytes_per_launch, flops_per_launch,
                                        args.profile_tag,
                                        limiter="issue latency: one chain's N_t-1 dependent steps on one CU "
