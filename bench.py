@@ -373,7 +373,14 @@ def bench_c4(args):
     u = np.random.default_rng(c["seed"]).uniform(2.0, 10.0, Nt)
     rows = list(range(1, Nt - 1))
 
+    KM = max(1, args.multi)
+    U_multi = np.stack([u] + [np.random.default_rng(c["seed"] + 1000 * k).uniform(2.0, 10.0, Nt)
+                              for k in range(1, KM)])
+
     def one():
+        if grad and KM > 1:   # K controls: one batch of 2K chains + batched divT / F
+            divT, F = eng.gradient_multi(U_multi)
+            return dt * (divT * F[:, None] * 1j).real
         if grad:
             eng.propagate(u, 3)
             divT = eng.div_t()
@@ -406,7 +413,7 @@ def bench_c4(args):
     done.set()
     gm = eng.stats(7)   # k_gemm: the MFMA-FP64 contraction kernel
     st_traj = eng.stats(0)
-    steps_traj = 2 * (Nt - 1)
+    steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
     row_steps = (Nt - 2) * (Nt - 3) // 2
     sweep = args.steps * (steps_traj + (0 if grad else row_steps))
     gemm_ms = gm["ms"] / max(1, gm["launches"])
@@ -414,7 +421,7 @@ def bench_c4(args):
         "metric": ("getAnalyticGradient/sec (psi || xi + divT)" if grad else "Hessian-rows/sec (getHessian fidelity part)")
                   + (", config 5 chain L=50 Npart=50 d=8 chi=512 tstep=0.01" if c5 else
                      ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005"),
-        "value": (args.steps if grad else args.steps * (Nt - 2)) / elapsed,
+        "value": (args.steps * KM if grad else args.steps * (Nt - 2)) / elapsed,
         "unit": "gradients/s" if grad else "rows/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c128/f64",

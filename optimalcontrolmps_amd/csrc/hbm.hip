@@ -1886,6 +1886,65 @@ int hbm_div_t(hbm_engine* h, double* divT) {
   });
 }
 
+// K controls' psi || xi in one lockstep batch of 2K chains, then their divT and F
+// in two batched overlap launches (ocg_gradient_multi).  Control 0 uses the
+// context's trajectory slots, control k >= 1 the 2N slots after xiH's block.
+// Every kernel is batch-independent: per control the numbers of
+// hbm_propagate(.., 3) + hbm_div_t + hbm_overlap_factor, bit for bit.
+int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* divT, double* F) {
+  return guard(h, [&] {
+    if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
+    hbm_prepare_N(h, N);
+    hbm::Engine& E = *h->E;
+    const int extra0 = h->xih_base() + N + 2;
+    auto pb = [&](int k) { return k == 0 ? h->psi_base() : extra0 + 2 * N * (k - 1); };
+    auto xb = [&](int k) { return k == 0 ? h->xi_base() : extra0 + 2 * N * (k - 1) + N; };
+    E.reserve_states(size_t(extra0) + size_t(2) * N * (K - 1));
+    E.reserve_chains(std::max(E.nchain_cap, 2 * K), false);
+    std::vector<Chain*> cs(2 * K);
+    std::vector<View> vs(2 * K);
+    std::vector<State*> ss(2 * K);
+    for (int k = 0; k < K; ++k) {
+      cs[2 * k] = E.acquire(false);
+      cs[2 * k + 1] = E.acquire(false);
+      vs[2 * k] = E.states[0].view();      // psi_init
+      vs[2 * k + 1] = E.states[1].view();  // psi_target
+      ss[2 * k] = &E.states[pb(k)];
+      ss[2 * k + 1] = &E.states[xb(k) + N - 1];
+    }
+    E.load_many(cs, vs);
+    E.store_many(ss, cs);
+    Timer t(h, 0);
+    std::vector<double> uf(2 * K), ut(2 * K);
+    std::vector<int> fw(2 * K);
+    for (int s = 0; s + 1 < N; ++s) {
+      for (int k = 0; k < K; ++k) {
+        const double* u = U + size_t(k) * N;
+        uf[2 * k] = u[s]; ut[2 * k] = u[s + 1]; fw[2 * k] = 1;
+        uf[2 * k + 1] = u[N - 1 - s]; ut[2 * k + 1] = u[N - 2 - s]; fw[2 * k + 1] = 0;
+        ss[2 * k] = &E.states[pb(k) + s + 1];
+        ss[2 * k + 1] = &E.states[xb(k) + N - 2 - s];
+      }
+      E.step(cs, uf, ut, fw);
+      E.store_many(ss, cs);
+    }
+    E.sync();
+    t.stop(long(2 * K) * (N - 1));
+    for (auto* c : cs) E.release(c);
+    h->have_psi = h->have_xi = true;
+    h->have_xih = false;
+    std::vector<int> xs(size_t(K) * N), ys(size_t(K) * N);
+    for (int k = 0; k < K; ++k)
+      for (int i = 0; i < N; ++i) { xs[size_t(k) * N + i] = xb(k) + i; ys[size_t(k) * N + i] = pb(k) + i; }
+    auto r = hbm_pairs(h, xs, ys, true);
+    for (size_t e = 0; e < size_t(K) * N; ++e) { divT[2 * e] = r[e].real(); divT[2 * e + 1] = r[e].imag(); }
+    std::vector<int> fx(K), fy(K, 1);
+    for (int k = 0; k < K; ++k) fx[k] = pb(k) + N - 1;
+    auto rf = hbm_pairs(h, fx, fy, false);
+    for (int k = 0; k < K; ++k) { F[2 * k] = rf[k].real(); F[2 * k + 1] = rf[k].imag(); }
+  });
+}
+
 // rows per batch of the Hessian / chunk of dH applications: bounded by memory
 static int hbm_batch(hbm_engine* h, int want) {
   hbm::Engine& E = *h->E;

@@ -37,6 +37,8 @@ int hbm_propagate(hbm_engine* h, const double* u, int N, int which);
 int hbm_overlap_factor(hbm_engine* h, double* F);
 int hbm_fidelities(hbm_engine* h, double* fid);
 int hbm_div_t(hbm_engine* h, double* divT);
+// K controls (rows of U) in one batch of 2K chains + batched divT / F (ocg_gradient_multi)
+int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* divT, double* F);
 int hbm_xi_dH(hbm_engine* h);
 int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int nrows, const double* F,
                      const double* divT, double* H);

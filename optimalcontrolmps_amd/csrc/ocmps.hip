@@ -943,6 +943,20 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
 int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, double* F) {
   if (!c || !u || !divT || !F || N < 2 || K < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
   if (size_t(K) * 4 * size_t(N) + 6 > size_t(INT32_MAX)) return fail(c, OCG_EINVAL, "K * N too large");
+  if (c->hbm && K > 1) {
+    // one batch of 2K chains when the extra trajectories fit half the free HBM, else in turn
+    size_t fr = 0, tot = 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemGetInfo(&fr, &tot));
+    const double per_control = hbm_traj_bytes(c->hbm, N) * (2.0 * N) / (3.0 * N + 6.0);
+    if (per_control * (K - 1) <= 0.5 * double(fr)) {
+      c->u_psi.clear();
+      c->u_xi.clear();
+      const int rc = hb(c, hbm_gradient_multi(c->hbm, K, u, N, divT, F));
+      if (!rc) note_u(c, u, N, 3);
+      return rc;
+    }
+  }
   if (c->hbm || K == 1) {  // controls in turn (last first: control 0's trajectories stay)
     for (int k = K - 1; k >= 0; --k) {
       if (int rc = ocg_propagate(c, u + size_t(k) * N, N, 3)) return rc;
