@@ -161,8 +161,12 @@ int ocg_hessian_multi(ocg_ctx* ctx, int K, const double* u, int N, const int* ro
  * calcFidelityGrad, src/OptimalControl.cpp:204-249) for K control vectors
  * u[k*N .. k*N+N) in one call: LDS engine, one trajectory launch of 2K chains
  * and one batched divT / F launch each (per control exactly the arithmetic of
- * ocg_propagate(..,3) + ocg_div_t + ocg_overlap_factor); HBM engine, the
- * controls in turn.  divT: K x 2N, F: K x 2; grad_k,i = dt Re(i divT_k,i F_k)
+ * ocg_propagate(..,3) + ocg_div_t + ocg_overlap_factor); HBM engine, one
+ * lockstep batch of 2K chains + one batched divT / F overlap launch each when
+ * the grown state heap (the context's slots + 2N per extra control) fits half
+ * the free HBM (the extra slots are released afterwards), else — or when the
+ * batched call fails to allocate — the controls in turn.  Either way the same
+ * numbers bit for bit.  divT: K x 2N, F: K x 2; grad_k,i = dt Re(i divT_k,i F_k)
  * (plus the caller's regularisation).  Leaves control 0's trajectories. */
 int ocg_gradient_multi(ocg_ctx* ctx, int K, const double* u, int N, double* divT, double* F);
 /* which: 0 psi_t, 1 xi_t, 2 xiHlist; copy trajectory state t to the host.
@@ -179,6 +183,21 @@ int ocg_get_state(ocg_ctx* ctx, int which, int t, int* dims, double* data, size_
  * sequential inner product in the reference's order without fused
  * multiply-adds: bit-identical to the host restatement.  Any engine. */
 int ocg_convert_hessian(ocg_ctx* ctx, const double* Hu, int N, const double* V, int M, double* Hc);
+
+/* ITensor denmatDecomp(M, A, B, Fromleft, {"Cutoff=",cutoff,"Maxm=",maxm})
+ * (called at src/BH_tDMRG.cpp:178, :191, :209) of nm independent dense
+ * blocks M[i] (rows[i] x cols[i] complex, row-major, 0 < rows <= cols <= any,
+ * rows <= 512), each one U(1) sector: the decomposition every two-site update
+ * of the HBM engine runs (Gram M M^H, Hermitian eigensolver, truncation rule,
+ * eigenvectors, factors), on caller-supplied matrices, batched in one pass.
+ * kept[i] = k; A[i] (rows x k, orthonormal columns) and B[i] = A^H M (k x
+ * cols), both row-major complex, caller buffers of rows*rows / rows*cols
+ * complex elements (NULL: not returned); w[i] (rows doubles, NULL: not
+ * returned) = the Gram eigenvalues as the eigensolver leaves them (order not
+ * specified; those below ~1e-3 cutoff / rows of the trace may be unresolved).
+ * HBM engine contexts only (ocg_create_ex engine 2); else OCG_EINVAL. */
+int ocg_denmat_decomp(ocg_ctx* ctx, int nm, const int* rows, const int* cols, const double* const* M,
+                      double cutoff, int maxm, int* kept, double* const* w, double* const* A, double* const* B);
 
 /* ------------------------------------------------------ instrumentation
  * Per-kernel HIP-event timing on the context's stream and the algorithmic

@@ -369,6 +369,14 @@ struct Engine {
     for (size_t i = 0; i < vec.size(); ++i)
       if (vec[i].get() == c) { (c->wide ? free_chain_w : free_chain).push_back(int(i)); return; }
   }
+  // Chains are held only inside one entry point: after a failed call every
+  // chain is free again (the error path of guard()).
+  void release_all() {
+    free_chain.clear();
+    free_chain_w.clear();
+    for (int i = nchain_cap - 1; i >= 0; --i) free_chain.push_back(i);
+    for (int i = nchain_cap_w - 1; i >= 0; --i) free_chain_w.push_back(i);
+  }
 
   // ------------------------------------------------------------ states
   void reserve_states(size_t nslots) {
@@ -391,6 +399,22 @@ struct Engine {
     }
     heap_slots = nslots;
   }
+  // Give back the slots past nslots (after a call that needed many extra
+  // trajectories): the first nslots keep their contents.
+  void shrink_states(size_t nslots) {
+    if (nslots >= heap_slots) return;
+    sync();
+    DBuf<z> nh;
+    nh.reserve(size_t(state_cap) * std::max<size_t>(nslots, 1));
+    if (nslots) HCK(hipMemcpyAsync(nh.p, heap.p, sizeof(z) * state_cap * nslots, hipMemcpyDeviceToDevice, st));
+    sync();
+    std::swap(heap.p, nh.p);
+    std::swap(heap.cap, nh.cap);
+    states.resize(nslots);
+    for (size_t s = 0; s < nslots; ++s) states[s].data = heap.p + size_t(state_cap) * s;
+    heap_slots = nslots;
+  }
+  double heap_bytes() const { return 16.0 * double(state_cap) * double(heap_slots); }
   void set_state_layout(State& s) {
     long o = 0;
     for (int k = 1; k <= L; ++k) {
@@ -869,6 +893,50 @@ struct Engine {
     }
     copy(ct);
     gemm(gt, gs);
+  }
+
+  // denmatDecomp(M, A, B, Fromleft, {Cutoff, Maxm}) of nm independent dense
+  // blocks (one U(1) sector each): the decomposition path every two-site
+  // update takes (Gram, eigenvalues, truncation, eigenvectors, factors), on
+  // caller-supplied matrices.  A = U (R x k, orthonormal columns), B = U^H M
+  // (k x C), w = the n = min(R, C) Gram eigenvalues as the eigensolver left
+  // them (those below thr_rel * trace may be unresolved; see EProb).
+  std::vector<int> decompose_dense(int nm, const int* rows, const int* cols, const double* const* M, double cutoff,
+                                   int maxm, double* const* w, double* const* X, double* const* Y) {
+    std::vector<DecompJob> jobs(static_cast<size_t>(nm));
+    const std::vector<int> bnd(Q1, 1 << 30);
+    for (int i = 0; i < nm; ++i) {
+      const int r = rows[i], c = cols[i];
+      z* d = walloc<z>(size_t(r) * c);
+      HCK(hipMemcpyAsync(d, M[i], sizeof(z) * size_t(r) * c, hipMemcpyHostToDevice, st));
+      QMat& Q = jobs[i].M;
+      Q.R.assign(Q1, 0);
+      Q.C.assign(Q1, 0);
+      Q.segs.assign(Q1, {});
+      Q.R[0] = r;
+      Q.C[0] = c;
+      Q.segs[0].push_back(Seg{d, c, 0, c});
+      jobs[i].dir = kFromleft;
+      jobs[i].cutoff = cutoff;
+      jobs[i].maxm = maxm;
+      jobs[i].normalize = 0;
+      jobs[i].bound = bnd.data();
+    }
+    EigRun R;
+    decompose_eig(jobs, R);
+    decompose_factors(jobs, R, {}, {});
+    std::vector<int> kept(static_cast<size_t>(nm), 0);
+    for (int i = 0; i < nm; ++i) {
+      const int k = jobs[i].kept[0], r = rows[i], c = cols[i];
+      kept[i] = k;
+      const EProb& P = R.probs[R.job_p0[i]];
+      if (w && w[i]) HCK(hipMemcpyAsync(w[i], P.w, sizeof(double) * P.n, hipMemcpyDeviceToHost, st));
+      if (k <= 0) continue;
+      if (X && X[i]) HCK(hipMemcpyAsync(X[i], jobs[i].X[0], sizeof(z) * size_t(r) * k, hipMemcpyDeviceToHost, st));
+      if (Y && Y[i]) HCK(hipMemcpyAsync(Y[i], jobs[i].Y[0], sizeof(z) * size_t(k) * c, hipMemcpyDeviceToHost, st));
+    }
+    sync();
+    return kept;
   }
 
   // ------------------------------------------------------------ matricisations
@@ -1635,19 +1703,28 @@ int widest_of(const hbm::Engine& E, const int* dims) {
   }
   return w;
 }
+// Every entry point runs inside guard(): exceptions become status codes, and a
+// failed call leaves no chain acquired (work already queued on the stream is
+// drained first, so a later call cannot reuse a buffer a kernel still writes).
+// Entry points that overwrite trajectory slots clear the matching have_* flags
+// before they start and set them only on success.
 template <class F>
 int guard(hbm_engine* h, F f) {
+  int rc = 0;
   try {
     HCK(hipSetDevice(h->E->device));
     f();
     return 0;
   } catch (const hbm::Error& e) {
     h->err = e.what();
-    return e.code;
+    rc = e.code;
   } catch (const std::exception& e) {
     h->err = e.what();
-    return 3;
+    rc = 3;
   }
+  (void)hipStreamSynchronize(h->E->st);
+  h->E->release_all();
+  return rc;
 }
 struct Timer {
   hbm_engine* h;
@@ -1813,6 +1890,8 @@ int hbm_propagate(hbm_engine* h, const double* u, int N, int which) {
   return guard(h, [&] {
     if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
     hbm_prepare_N(h, N);
+    if (which & 1) h->have_psi = false;
+    if (which & 2) h->have_xi = h->have_xih = false;
     hbm::Engine& E = *h->E;
     E.reserve_chains(std::max(E.nchain_cap, 2), false);
     std::vector<Chain*> cs;
@@ -1895,6 +1974,7 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
   return guard(h, [&] {
     if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
     hbm_prepare_N(h, N);
+    h->have_psi = h->have_xi = h->have_xih = false;
     hbm::Engine& E = *h->E;
     const int extra0 = h->xih_base() + N + 2;
     auto pb = [&](int k) { return k == 0 ? h->psi_base() : extra0 + 2 * N * (k - 1); };
@@ -1942,6 +2022,9 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
     for (int k = 0; k < K; ++k) fx[k] = pb(k) + N - 1;
     auto rf = hbm_pairs(h, fx, fy, false);
     for (int k = 0; k < K; ++k) { F[2 * k] = rf[k].real(); F[2 * k + 1] = rf[k].imag(); }
+    // the other controls' trajectories are not kept: give their slots back so the
+    // free-memory checks of later calls (checkpointing, row batches) see them
+    E.shrink_states(size_t(extra0));
   });
 }
 
@@ -1959,6 +2042,7 @@ static int hbm_batch(hbm_engine* h, int want) {
 int hbm_xi_dH(hbm_engine* h) {
   return guard(h, [&] {
     if (!h->have_xi) throw hbm::Error(4, "xi_t not propagated");
+    h->have_xih = false;
     hbm::Engine& E = *h->E;
     const int N = h->N;
     const int B = hbm_batch(h, N);
@@ -2275,3 +2359,14 @@ bool hbm_have(const hbm_engine* h, int what) {
   return false;
 }
 int hbm_N(const hbm_engine* h) { return h->N; }
+
+int hbm_denmat_decomp(hbm_engine* h, int nm, const int* rows, const int* cols, const double* const* M, double cutoff,
+                      int maxm, int* kept, double* const* w, double* const* X, double* const* Y) {
+  return guard(h, [&] {
+    for (int i = 0; i < nm; ++i)
+      if (rows[i] <= 0 || cols[i] <= 0 || rows[i] > cols[i] || rows[i] > hbm::kBtRows)
+        throw hbm::Error(1, "block shape: need 0 < rows <= cols and rows <= 512");
+    const auto k = h->E->decompose_dense(nm, rows, cols, M, cutoff, maxm > 0 ? maxm : 5000, w, X, Y);
+    for (int i = 0; i < nm; ++i) kept[i] = k[i];
+  });
+}

@@ -58,3 +58,6 @@ int hbm_stats(hbm_engine* h, int kind, double* ms, long* launches, double* bytes
 void hbm_reset_stats(hbm_engine* h);
 bool hbm_have(const hbm_engine* h, int what);  // 0 states, 1 psi, 2 xi, 3 xiH
 int hbm_N(const hbm_engine* h);
+// denmatDecomp (Fromleft) of nm independent dense blocks (ocg_denmat_decomp)
+int hbm_denmat_decomp(hbm_engine* h, int nm, const int* rows, const int* cols, const double* const* M, double cutoff,
+                      int maxm, int* kept, double* const* w, double* const* X, double* const* Y);

@@ -224,6 +224,7 @@ struct ocg_ctx {
   size_t rs_cap = 0;
   int* d_flags = nullptr;     // [2N] psi / xi publication epochs
   int flags_cap = 0;
+  int flags_N = -1, flags_K = -1;  // (N, K) layout of the flag buffer's current epoch run
   int epoch = 0;
   int* d_err = nullptr;
   int* d_rows = nullptr;      // rows, then rbase (nrows + 1)
@@ -944,20 +945,38 @@ int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, 
   if (!c || !u || !divT || !F || N < 2 || K < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
   if (size_t(K) * 4 * size_t(N) + 6 > size_t(INT32_MAX)) return fail(c, OCG_EINVAL, "K * N too large");
   if (c->hbm && K > 1) {
-    // one batch of 2K chains when the extra trajectories fit half the free HBM, else in turn
+    // One batch of 2K chains when the grown state heap fits half the free HBM,
+    // else in turn.  The heap grows by copying into a new allocation while the
+    // old one is live, so the whole new heap (the context's own 3N + 6 slots +
+    // 2N per extra control) must fit in the free memory; the extra slots are
+    // given back after the call (hbm_gradient_multi).  A batched call that
+    // still fails (allocation) falls back to the in-turn loop.
     size_t fr = 0, tot = 0;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemGetInfo(&fr, &tot));
-    const double per_control = hbm_traj_bytes(c->hbm, N) * (2.0 * N) / (3.0 * N + 6.0);
-    if (per_control * (K - 1) <= 0.5 * double(fr)) {
+    const double base = hbm_traj_bytes(c->hbm, N);
+    const double per_control = base * (2.0 * N) / (3.0 * N + 6.0);
+    if (base + per_control * (K - 1) <= 0.5 * double(fr)) {
       c->u_psi.clear();
       c->u_xi.clear();
-      const int rc = hb(c, hbm_gradient_multi(c->hbm, K, u, N, divT, F));
-      if (!rc) note_u(c, u, N, 3);
-      return rc;
+      if (hb(c, hbm_gradient_multi(c->hbm, K, u, N, divT, F)) == 0) {
+        note_u(c, u, N, 3);
+        return 0;
+      }
     }
   }
-  if (c->hbm || K == 1) {  // controls in turn (last first: control 0's trajectories stay)
+  // LDS engine: control k's psi / xi at slot stride 2N (psi_t, xi_t only; control
+  // 1's psi_t takes control 0's xiH_t slots, which this call invalidates anyway).
+  // The slot pool must fit half the free HBM, else the controls run in turn.
+  bool lds_batch = !c->hbm && K > 1;
+  if (lds_batch) {
+    size_t fr = 0, tot = 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemGetInfo(&fr, &tot));
+    const double need = (6.0 + 2.0 * N * K) * (sizeof(zc) * double(c->P.cap) + sizeof(int) * double(c->P.nsq));
+    lds_batch = 6 + 2 * N * K <= c->nslots || need <= 0.5 * double(fr);  // growth copies: old + new live
+  }
+  if (!lds_batch) {  // controls in turn (last first: control 0's trajectories stay)
     for (int k = K - 1; k >= 0; --k) {
       if (int rc = ocg_propagate(c, u + size_t(k) * N, N, 3)) return rc;
       if (int rc = ocg_div_t(c, divT + size_t(k) * 2 * N)) return rc;
@@ -974,7 +993,7 @@ int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, 
   }
   c->u_psi.clear();
   c->u_xi.clear();
-  const int cs = 4 * N;  // slot stride between controls (as ocg_hessian_multi)
+  const int cs = 2 * N;  // slot stride between controls: psi_t, xi_t
   if (int rc = ensure_slots(c, 6 + cs * K)) return rc;
   if (int rc = ensure_buf(c, c->d_u, c->u_cap, K * N)) return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * K * N, hipMemcpyHostToDevice, c->stream));
@@ -1196,14 +1215,22 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   if (int rc = ensure_buf(c, c->d_rows, c->rows_cap, 2 * nrows + 2)) return rc;
   if (int rc = ensure_buf(c, c->d_prn, c->prn_cap, K * nrows + 1)) return rc;
   const int nflags = K * (2 * N + 2) + 1;  // K blocks (psi / xi flags, progress, spare) + the ticket counter
-  if (nflags > c->flags_cap) {  // publication flags (+ progress counter) start at 0 (< any epoch)
+  if (nflags > c->flags_cap) {
     if (c->d_flags) (void)hipFree(c->d_flags);
     c->d_flags = nullptr;
     c->flags_cap = 0;
     if (int rc = ensure_buf(c, c->d_flags, c->flags_cap, nflags)) return rc;
+    c->flags_N = -1;
+  }
+  // Publication flags hold epochs; each control's progress counter and the
+  // ticket counter share the buffer at positions that depend on (N, K).  When
+  // the layout changes, a stale counter could sit where a flag now lives and
+  // read as already published, so the whole prefix restarts at 0 (< any epoch).
+  if (c->flags_N != N || c->flags_K != K) {
     HIPCHK(c, hipMemsetAsync(c->d_flags, 0, sizeof(int) * c->flags_cap, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->epoch = 0;
+    c->flags_N = N;
+    c->flags_K = K;
   }
   // stored row states: row i keeps psiH_i(j), j = i..N-2 (O(N^2) states).
   // Past the memory budget (or int offsets) the unfused path runs instead:
@@ -1406,6 +1433,15 @@ int ocg_convert_hessian(ocg_ctx* c, const double* Hu, int N, const double* V, in
   HIPCHK(c, hipMemcpyAsync(Hc, dHc, sizeof(double) * M * M, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
+}
+
+int ocg_denmat_decomp(ocg_ctx* c, int nm, const int* rows, const int* cols, const double* const* M, double cutoff,
+                      int maxm, int* kept, double* const* w, double* const* A, double* const* B) {
+  if (!c || nm < 0 || (nm > 0 && (!rows || !cols || !M || !kept)))
+    return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (!c->hbm) return fail(c, OCG_EINVAL, "ocg_denmat_decomp: HBM engine contexts only (ocg_create_ex engine 2)");
+  if (nm == 0) return 0;
+  return hb(c, hbm_denmat_decomp(c->hbm, nm, rows, cols, M, cutoff, maxm, kept, w, A, B));
 }
 
 int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t cap, size_t* nelem) {

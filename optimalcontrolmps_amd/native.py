@@ -113,6 +113,8 @@ SIGNATURES = [
     ("ocg_gradient_multi", C.c_int, [C.c_void_p, C.c_int, dp, C.c_int, dp, dp]),
     ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_convert_hessian", C.c_int, [C.c_void_p, dp, C.c_int, dp, C.c_int, dp]),
+    ("ocg_denmat_decomp", C.c_int, [C.c_void_p, C.c_int, ip, ip, C.POINTER(dp), C.c_double, C.c_int, ip,
+                                    C.POINTER(dp), C.POINTER(dp), C.POINTER(dp)]),
     ("ocg_kernel_stats", C.c_int, [C.c_void_p, C.c_int, dp, C.POINTER(C.c_long), dp, dp, C.POINTER(C.c_long)]),
     ("ocg_reset_stats", C.c_int, [C.c_void_p]),
     ("ocg_profile", C.c_int, [C.c_void_p, dp, C.c_int]),
@@ -372,6 +374,31 @@ class Engine:
         M, N = Vm.shape
         out = np.zeros((M, M))
         self._chk(lib().ocg_convert_hessian(self.h, ph, N, pv, M, out.ctypes.data_as(dp)), "ocg_convert_hessian")
+        return out
+
+    def denmat_decomp(self, mats, cutoff=None, maxm=None):
+        """ITensor denmatDecomp (Fromleft) of independent dense complex blocks
+        (rows <= cols <= any, rows <= 512) through the HBM engine's batched
+        decomposition path (ocg_denmat_decomp): returns [(k, w, A, B)] with A
+        (rows x k, orthonormal columns), B = A^H M (k x cols) and the rows Gram
+        eigenvalues w as the eigensolver left them."""
+        n = len(mats)
+        Ms = [np.ascontiguousarray(np.asarray(m, np.complex128)) for m in mats]
+        rows, pr = _i([m.shape[0] for m in Ms])
+        cols, pc = _i([m.shape[1] for m in Ms])
+        ws = [np.zeros(m.shape[0]) for m in Ms]
+        As = [np.zeros(2 * m.shape[0] * m.shape[0]) for m in Ms]
+        Bs = [np.zeros(2 * m.shape[0] * m.shape[1]) for m in Ms]
+        arr = lambda xs: (dp * n)(*[x.view(np.float64).ctypes.data_as(dp) for x in xs])
+        kept = np.zeros(n, np.int32)
+        self._chk(lib().ocg_denmat_decomp(self.h, n, pr, pc, arr(Ms), self.cutoff if cutoff is None else cutoff,
+                                          self.maxm if maxm is None else maxm, kept.ctypes.data_as(ip), arr(ws),
+                                          arr(As), arr(Bs)), "ocg_denmat_decomp")
+        out = []
+        for i, m in enumerate(Ms):
+            k, r, c = int(kept[i]), m.shape[0], m.shape[1]
+            out.append((k, ws[i], As[i].view(np.complex128)[:r * k].reshape(r, k),
+                        Bs[i].view(np.complex128)[:k * c].reshape(k, c)))
         return out
 
     def state(self, which, t) -> MPS:

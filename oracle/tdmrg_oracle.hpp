@@ -876,9 +876,18 @@ struct OC {
   }
 
   // calcHessian_parallel / _sequencial (:281-372), row-major N x N.
+  // threads > 1: psi and xi on two threads (calcPsiXiDivT, :424-430) and the
+  // xiH list by the worker pool (the reference builds it serially, :300-303;
+  // every entry is computed independently, so the result is the same).
   std::vector<double> hessian(const std::vector<double>& u, int threads) {
-    calcPsi(u);
-    calcXi(u);
+    if (threads > 1) {
+      std::thread tx([&]() { calcXi(u); });
+      calcPsi(u);
+      tx.join();
+    } else {
+      calcPsi(u);
+      calcXi(u);
+    }
     calcDivT();
     std::vector<double> H(N * N, 0.0);
     double g = gamma / st.dt;  // calcRegularizationHessian (:124-143)
@@ -886,7 +895,17 @@ struct OC {
     H[1 * N + 0] = 0; H[(N - 2) * N + N - 1] = 0;
     cplx F = overlapFactor();
     xiH.assign(N, MPS());
-    for (size_t i = 0; i < N; ++i) xiH[i] = st.apply_dH(xi_t[i]);
+    if (threads > 1) {
+      std::atomic<size_t> next(0);
+      std::vector<std::thread> pool;
+      for (int t = 0; t < threads; ++t)
+        pool.emplace_back([&]() {
+          for (size_t i; (i = next.fetch_add(1)) < N;) xiH[i] = st.apply_dH(xi_t[i]);
+        });
+      for (auto& th : pool) th.join();
+    } else {
+      for (size_t i = 0; i < N; ++i) xiH[i] = st.apply_dH(xi_t[i]);
+    }
     rows(u, F, H, threads);
     return H;
   }

@@ -12,7 +12,9 @@ c4.npz:
           evolved 400 steps at U = 2.5 on the GPU engine, bonds saturated at
           256); one oracle step u 2.5 -> 3.0 forward: bond dims, <psi_0|psi_1>,
           <psi_1|dH|psi_1>.
-Run: python tests/golden/make_c4_fixtures.py [s32] [w256]
+  w256h/* Maxm = 256, N_t = 5: gradient and full fidelity Hessian from the
+          saturated warm state (make_w256h).
+Run: python tests/golden/make_c4_fixtures.py [s32] [w256] [w256h]
 """
 import os
 import sys
@@ -71,6 +73,32 @@ def make_w256(out):
                 "w256/dH11": np.array([dh])})
 
 
+def make_w256h(out, Nt=5):
+    """w256h/*: config 4's real bond dimension (Maxm 256) from the saturated
+    warm state: psi_target = psi_init stepped once at U = 6 (an overlapping
+    target, see make_s32), N_t = 5 GRAPE controls U(2,10) (seed 5256): divT, F,
+    the GRAPE gradient (gamma = 0: dt Re(divT_i F i), calcFidelityGrad
+    src/OptimalControl.cpp:240-246) and the full fidelity Hessian (rows 1..3,
+    calcHessianRow :251-279) on the oracle with psi || xi and the row pool on
+    8 threads (~1 h on this container)."""
+    z = np.load(os.path.join(HERE, "c4_warm256.npz"), allow_pickle=False)
+    st = O.Stepper(L, p, N, J, DT, CUT, 256)
+    psi0 = O.MPS(L, p, N, z["dims"], z["data"])
+    t0 = time.time()
+    tgt = st.step(psi0, 6.0, 6.0, True)
+    print(f"w256h target {time.time() - t0:.1f}s bonds {list(tgt.bond_dims())}", flush=True)
+    u = np.random.default_rng(5256).uniform(2.0, 10.0, Nt)
+    oc = O.OC(st, tgt, psi0, Nt, 0.0)
+    t0 = time.time()
+    H = oc.hessian(u, 8)
+    divT, F = oc.divT_F()
+    g = DT * (divT * F * 1j).real
+    print(f"w256h oracle hessian {time.time() - t0:.1f}s  max|H| {np.abs(H).max():.3e} "
+          f"max|g| {np.abs(g).max():.3e} F {F}", flush=True)
+    out.update({"w256h/tgt_dims": tgt.dims, "w256h/tgt_data": tgt.data, "w256h/u": u, "w256h/H": H,
+                "w256h/grad": g, "w256h/divT": divT, "w256h/F": np.array([F])})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["s32", "w256"]
     out = load_out()
@@ -78,4 +106,6 @@ if __name__ == "__main__":
         make_s32(out)
     if "w256" in which:
         make_w256(out)
+    if "w256h" in which:
+        make_w256h(out)
     np.savez_compressed(OUT, **out)

@@ -1,0 +1,97 @@
+"""The HBM engine's decomposition path (Gram -> Hermitian eigensolver ->
+truncation -> eigenvectors -> factors: ITensor denmatDecomp, called at
+src/BH_tDMRG.cpp:178, :191, :209) on caller-supplied blocks through
+ocg_denmat_decomp, against numpy's SVD (an independent LAPACK result).
+
+Config 5 (chi = 512, p = 9) produces Gram blocks of order 209..512, which run
+on the blocked kernels (k_heev_vals_big, k_heev_bt / CholeskyQR2); the config
+tests at Maxm 16/32 never reach them.  Checked per block, all gauge-invariant:
+* kept count = the truncation rule on numpy's spectrum (oracle truncate_count:
+  discard the smallest while their sum < cutoff * total, cap Maxm);
+* resolved eigenvalues = numpy's squared singular values (1e-12 of the largest);
+* A has orthonormal columns (1e-11);
+* A B = the best rank-k approximation of M (1e-9 of ||M||_F: the Gram route
+  resolves directions of singular value s to ~eps s_max^2 / s^2).
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+L, p, NPART = 20, 7, 20   # an HBM-engine context (the chain shape does not enter)
+
+
+def block(rng, n, c, spec, rank=None):
+    """n x c complex with singular values spec (length min(n, c) or rank)"""
+    r = len(spec) if rank is None else rank
+    U, _ = np.linalg.qr(rng.normal(size=(n, r)) + 1j * rng.normal(size=(n, r)))
+    V, _ = np.linalg.qr(rng.normal(size=(c, r)) + 1j * rng.normal(size=(c, r)))
+    return (U * np.asarray(spec[:r])) @ V.conj().T
+
+
+def check(M, res, cutoff, maxm):
+    k, w, A, B = res
+    s = np.linalg.svd(M, compute_uv=False)
+    lam = s ** 2
+    k_ref = O.truncate(lam, cutoff, maxm)
+    assert k == k_ref, (M.shape, k, k_ref)
+    # resolved eigenvalues (the kept ones and every one above the unresolved threshold)
+    wd = np.sort(w)[::-1]
+    assert np.abs(wd[:k] - lam[:k]).max() <= 1e-12 * lam[0], M.shape
+    assert np.abs(A.conj().T @ A - np.eye(k)).max() <= 1e-11, M.shape
+    U, s2, Vh = np.linalg.svd(M, full_matrices=False)
+    Mk = (U[:, :k] * s2[:k]) @ Vh[:k]
+    assert np.linalg.norm(A @ B - Mk) <= 1e-9 * np.linalg.norm(M), M.shape
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from optimalcontrolmps_amd.native import Engine
+    e = Engine(L, p, NPART, 1.0, 0.005, 1e-8, 512, engine="hbm")
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("n,c", [(209, 240), (256, 256), (320, 448), (448, 560), (512, 512)])
+def test_blocked_orders_vs_numpy(eng, n, c):
+    """one block per call on the blocked large-order path, geometric spectrum
+    (cutoff 1e-8 keeps ~90 of n)"""
+    rng = np.random.default_rng(n * 1000 + c)
+    spec = np.exp(-np.arange(n) / 5.0)
+    M = block(rng, n, c, spec)
+    check(M, eng.denmat_decomp([M], 1e-8, 512)[0], 1e-8, 512)
+
+
+def test_mixed_orders_one_batch(eng):
+    """register, LDS and blocked kernels in one decomposition pass (the blocked
+    one on the side stream), slow spectra so that Maxm binds on the big ones"""
+    rng = np.random.default_rng(77)
+    shapes = [(12, 30), (48, 64), (130, 200), (208, 208), (209, 300), (300, 300), (512, 700)]
+    Ms = [block(rng, n, c, 1.0 / (1.0 + np.arange(n)) ** 1.5) for n, c in shapes]
+    res = eng.denmat_decomp(Ms, 1e-8, 128)
+    for M, r in zip(Ms, res):
+        check(M, r, 1e-8, 128)
+    assert max(r[0] for r in res) == 128
+
+
+def test_rank_deficient_and_clustered(eng):
+    """exact null space (rank 100 of order 300) and a degenerate cluster inside
+    the kept set (k_heev_vecs / CholeskyQR2 on repeated eigenvalues)"""
+    rng = np.random.default_rng(5)
+    M1 = block(rng, 300, 320, np.exp(-np.arange(100) / 10.0), rank=100)
+    spec = np.exp(-np.arange(450) / 6.0)
+    spec[3:9] = spec[3]  # six-fold degenerate singular value
+    M2 = block(rng, 450, 450, spec)
+    res = eng.denmat_decomp([M1, M2], 1e-8, 512)
+    check(M1, res[0], 1e-8, 512)
+    check(M2, res[1], 1e-8, 512)
+
+
+def test_lds_engine_refuses(states):
+    from optimalcontrolmps_amd.native import Engine, OcgError
+    e = Engine(5, 5, 5, 1.0, 0.01, 1e-8, 80, engine="lds")
+    with pytest.raises(OcgError):
+        e.denmat_decomp([np.eye(4, dtype=complex)])
+    e.close()

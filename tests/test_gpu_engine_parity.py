@@ -370,3 +370,24 @@ def test_gradient_multi_equals_single(states, K):
         assert np.array_equal(dm[k], eng.div_t()) and Fm[k] == eng.overlap_factor(), k
         if k == 0:
             assert np.array_equal(fid_m, eng.fidelities())
+
+
+def test_flag_layout_change_between_launches(states):
+    """ocg_hessian on one context at N_t = 201, then 101, then 201 (and a K = 2
+    multi launch in between): the flag buffer's per-control progress and ticket
+    counters move with (N, K), so stale counters must never read as published
+    flags.  The last Hessian equals a fresh context's bit for bit."""
+    L, p, N, J = 5, 5, 5, 1.0
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    rng = np.random.default_rng(1201)
+    u201, u101 = rng.uniform(2, 10, 201), rng.uniform(2, 10, 101)
+    eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+    eng.set_states(tgt, ini)
+    eng.hessian(u201)
+    eng.hessian(u101)
+    eng.hessian_multi(rng.uniform(2, 10, (2, 101)))
+    H3, d3, F3 = eng.hessian(u201)
+    fresh = engine(L, p, N, J, 0.01, 1e-8, 80)
+    fresh.set_states(tgt, ini)
+    H0, d0, F0 = fresh.hessian(u201)
+    assert np.array_equal(H3, H0) and np.array_equal(d3, d0) and F3 == F0
