@@ -59,7 +59,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=8)
-    ap.add_argument("--mode", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--mode", choices=["weak", "strong"], default=None,
+                    help="weak: every rank its own getHessian; strong: one getHessian's rows over the ranks "
+                         "(default: weak for config 1, strong for c4rows / c5rows)")
+    ap.add_argument("--group-m", type=int, default=40, help="GROUP basis size of the c4rows workload (0: GRAPE)")
     ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c4rows", "c5rows"], default="hessian")
     ap.add_argument("--c4-nt", type=int, default=33)
     ap.add_argument("--c5-nt", type=int, default=5)
@@ -70,7 +73,7 @@ def main():
     ap.add_argument("--multi", type=int, default=1,
                     help="K control vectors per GPU in one ocg_hessian_multi call (one pipeline launch for all K); "
                          "value = rows of all K per second")
-    ap.add_argument("--profile-tag", default="r02")
+    ap.add_argument("--profile-tag", default="r03")
     args = ap.parse_args()
     if args.workload in ("c4grad", "c4rows", "c5rows"):
         return bench_c4(args)
@@ -102,6 +105,7 @@ def main():
     ini = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, CFG["U_init"])[0], L, p, Q))
     tgt = MPS(L, p, Q, *ed.mps_from_full(ed.ground_state_full(L, p, Q, J, CFG["U_target"])[0], L, p, Q))
     strong = args.mode == "strong"
+    args.mode = args.mode or "weak"
     # weak: rank r evaluates its own control vector (seed + r); strong: one shared vector
     u = np.random.default_rng(CFG["seed"] + (0 if strong else rank)).uniform(2.0, 10.0, Nt)
     rows = zigzag_rows(Nt - 2, rank, world) if strong else list(range(1, Nt - 1))
@@ -229,7 +233,7 @@ def main():
             "roofline": roofline_block("k_pipeline", launch_ms, bytes_per_launch, flops_per_launch,
                                        args.profile_tag,
                                        limiter="issue latency: one chain's N_t-1 dependent steps on one CU "
-                                               "(state in LDS); HBM and FP64 are both <1% busy"),
+                                               "(state in LDS); HBM and FP64 are both <1% busy", bound="latency"),
         }
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(ini, tgt, u, args.cpu_threads)
@@ -250,9 +254,12 @@ def st_traj_ms_per_step(eng, Nt):
 
 def roofline_block(kernel, launch_ms, bytes_per_launch, flops_per_launch, tag, limiter, bound="hbm"):
     """Roofline of the dominant kernel.  achieved = algorithmic bytes (SURVEY.md
-    §8d model) / HIP-event launch time; traffic = HBM bytes
-    per dispatch measured by rocprofv3 PMC (profiles/<tag>_summary.json, FETCH_SIZE
-    doubled per the gfx950 calibration) and its own fraction of peak."""
+    §8d model) / HIP-event launch time, priced against the
+    HBM peak; `bound` names what really limits the kernel ("latency": dependent
+    instruction chains, neither HBM nor the MFMA pipes).  traffic = HBM bytes per
+    dispatch measured by rocprofv3 PMC over THIS workload's command
+    (profiles/<tag>_summary.json, tag = round + workload + N_t; FETCH_SIZE
+    doubled per the gfx950 calibration), null when no such profile exists."""
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     traffic = measured_traffic(kernel, tag)
     meas = traffic / (launch_ms * 1e-3) / 1e9 if (traffic and launch_ms > 0) else None
@@ -324,8 +331,9 @@ def bench_gradient(args, eng, u, Nt, dt, world, rank, dist, cdev, U_multi):
             "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(launch_ms, 1e-9),
             "kernels": {"trajectory_ms": launch_ms, "divT_F_ms": st_ov["ms"] / max(1, args.steps)},
             "roofline": roofline_block("k_trajectory", launch_ms, st_traj["alg_bytes"] / max(1, st_traj["launches"]),
-                                       st_traj["alg_flops"] / max(1, st_traj["launches"]), args.profile_tag,
-                                       limiter="issue latency: 200 dependent steps per chain, one CU per chain"),
+                                       st_traj["alg_flops"] / max(1, st_traj["launches"]), args.profile_tag + "grad",
+                                       limiter="issue latency: 200 dependent steps per chain, one CU per chain",
+                                       bound="latency"),
         }
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -339,24 +347,51 @@ C5 = dict(L=50, p=9, npart=50, J=1.0, tstep=0.01, T=10.0, maxm=512, cutoff=1e-8,
 
 def bench_c4(args):
     """Config 4's chain (BASELINE configs[3]: L=20 Npart=20 d=6 chi=256 tstep=0.005
-    T=4) on the HBM-resident engine, one GPU.  psi_init = the saturated warm state
-    (tests/golden/c4_warm256.npz: |1..1> evolved 400 steps at U=2.5, bonds 256),
-    psi_target = psi_init evolved 2 more steps at U=6 (config 4's |1..1> target has
-    ~1e-10 overlap, which leaves every derivative at rounding level; cost is
-    independent of the target).  GRAPE controls U(2,10); the GROUP M=40 projection
-    is a host GEMM (ControlBasis) and not part of the timed device work.
+    T=4, GROUP M=40, 8 GPUs) and config 5's (configs[4]: L=50 Npart=50 d=8
+    chi=512 tstep=0.01, 1/2/4/8 GPUs) on the HBM-resident engine.
 
-    c5rows: config 5's chain (BASELINE configs[4]: L=50 Npart=50 d=8 chi=512
-    tstep=0.01): psi_init = the Mott state |1..1> evolved --c5-warm steps at U=2.5
-    on the device (untimed; the bonds saturate at 512 after ~220 steps), a
-    getHessian slice of --c5-nt time points (the aspirational scaling slice of
-    SURVEY.md §8d)."""
+    c4rows: one getHessian per step over a T slice of --c4-nt time points
+      (default 33: 31 rows): GROUP M=40 (chopped-sine basis over the slice, u0 =
+      the adiabatic seed 2 -> 10, coefficients c ~ U(-2,2), a new draw per step
+      so every step is a fresh getHessian(c, new_control=true)): convertControl
+      on the host, the rows of H_u dealt zig-zag over the ranks (each rank
+      recomputes psi, xi, divT, xiH), one RCCL reduce onto rank 0, the
+      regularisation Hessian (gamma 1e-6) and H_c = V H_u V^T on rank 0's device
+      (ocg_convert_hessian).  psi_init = the saturated warm state
+      (tests/golden/c4_warm256.npz: |1..1> evolved 400 steps at U=2.5, bonds
+      256), psi_target = psi_init evolved 2 more steps at U=6 (config 4's |1..1>
+      target has ~1e-10 overlap, which leaves every derivative at rounding
+      level; cost is independent of the target).
+    c5rows: the same over --c5-nt time points of config 5's chain, GRAPE
+      controls U(2,10), psi_init = the Mott state |1..1> evolved --c5-warm steps
+      at U=2.5 on each rank's device (untimed; the bonds saturate at 512 after
+      ~220 steps).
+    c4grad: one getAnalyticGradient over the full horizon (N_t=801) per rank
+      (the gradient's time recursion does not shard: replicas).
+
+    --mode strong (default for c4rows/c5rows): one Hessian's rows over all
+    ranks; --mode weak: every rank a whole Hessian of its own control."""
     import torch
+    from optimalcontrolmps_amd.control_basis import adiabatic_seed, build_chopped_sine_basis
+    from optimalcontrolmps_amd.distributed import sharded_hessian, torch_reduce
     from optimalcontrolmps_amd.native import MPS, Engine
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("OCG_BENCH_BACKEND", "nccl")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    cdev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
     c5 = args.workload == "c5rows"
+    grad = args.workload == "c4grad"
+    strong = (args.mode or ("weak" if grad else "strong")) == "strong" and not grad
     c = C5 if c5 else C4
     L, p, Q, dt = c["L"], c["p"], c["npart"], c["tstep"]
-    eng = Engine(L, p, Q, c["J"], dt, c["cutoff"], c["maxm"], device=0, engine="hbm")
+    eng = Engine(L, p, Q, c["J"], dt, c["cutoff"], c["maxm"], device=local, engine="hbm")
     if c5:
         from optimalcontrolmps_amd.states import product_state, warm_state
         t0 = time.perf_counter()
@@ -368,29 +403,37 @@ def bench_c4(args):
         warm_s = 0.0
     tgt = eng.steps(ini, np.full(3, 6.0), True)
     eng.set_states(tgt, ini)
-    grad = args.workload == "c4grad"
     Nt = int(round(c["T"] / dt)) + 1 if grad else (args.c5_nt if c5 else args.c4_nt)
-    u = np.random.default_rng(c["seed"]).uniform(2.0, 10.0, Nt)
-    rows = list(range(1, Nt - 1))
+    M = 0 if (grad or c5) else args.group_m
+    gamma = 1e-6 if M else 0.0
+    basis = build_chopped_sine_basis(adiabatic_seed(2.0, 10.0, Nt), dt, (Nt - 1) * dt, M) if M else None
+    nsteps_all = args.warmup + args.steps
+    seed = c["seed"] + (0 if strong else 7919 * rank)
 
+    def control(s):   # a fresh control vector per step (every getHessian has new_control = true)
+        rng = np.random.default_rng(seed + 1000 * s)
+        if basis is not None:
+            return basis.convert_control(rng.uniform(-2.0, 2.0, M))
+        return rng.uniform(2.0, 10.0, Nt)
     KM = max(1, args.multi)
-    U_multi = np.stack([u] + [np.random.default_rng(c["seed"] + 1000 * k).uniform(2.0, 10.0, Nt)
-                              for k in range(1, KM)])
+    reduce = torch_reduce(dist, cdev, Nt) if (world > 1 and strong) else None
+    project = (lambda Hu: eng.convert_hessian(Hu, basis.V)) if basis is not None else None
 
-    def one():
-        if grad and KM > 1:   # K controls: one batch of 2K chains + batched divT / F
-            divT, F = eng.gradient_multi(U_multi)
-            return dt * (divT * F[:, None] * 1j).real
+    def one(s):
         if grad:
+            if KM > 1:   # K controls: one batch of 2K chains + batched divT / F
+                Um = np.stack([control(s * KM + k) for k in range(KM)])
+                divT, F = eng.gradient_multi(Um)
+                return dt * (divT * F[:, None] * 1j).real
+            u = control(s)
             eng.propagate(u, 3)
             divT = eng.div_t()
             F = eng.overlap_factor()
             return dt * (divT * F * 1j).real
-        eng.propagate(u, 3)
-        divT = eng.div_t()
-        F = eng.overlap_factor()
-        eng.xi_dH()
-        return eng.hessian_rows(u, rows, F, divT)
+        u = control(s)   # GROUP: convertControl (src/ControlBasis.cpp:49-67), host
+        H, divT, F, _ = sharded_hessian(lambda uu, rows: eng.hessian(uu, rows), u, rank if strong else 0,
+                                        world if strong else 1, reduce, gamma=gamma, tstep=dt, project=project)
+        return H
 
     import threading
     done = threading.Event()
@@ -401,49 +444,70 @@ def bench_c4(args):
             print(f"[bench] {args.workload} N_t={Nt}: {time.perf_counter() - t_hb:.0f} s", file=sys.stderr, flush=True)
 
     threading.Thread(target=heartbeat, daemon=True).start()
-    for _ in range(args.warmup):
-        one()
+    for s in range(args.warmup):
+        one(s)
     eng.reset_stats()
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one()
+    for s in range(args.warmup, nsteps_all):
+        one(s)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
     done.set()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
     gm = eng.stats(7)   # k_gemm: the MFMA-FP64 contraction kernel
     st_traj = eng.stats(0)
     steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
     row_steps = (Nt - 2) * (Nt - 3) // 2
-    sweep = args.steps * (steps_traj + (0 if grad else row_steps))
+    reps = 1 if strong else world   # independent Hessians / gradients per step
+    sweep = args.steps * (steps_traj * (world if (strong or grad) else reps) + (0 if grad else row_steps * reps))
     gemm_ms = gm["ms"] / max(1, gm["launches"])
-    res = {
-        "metric": ("getAnalyticGradient/sec (psi || xi + divT)" if grad else "Hessian-rows/sec (getHessian fidelity part)")
-                  + (", config 5 chain L=50 Npart=50 d=8 chi=512 tstep=0.01" if c5 else
-                     ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005"),
-        "value": (args.steps * KM if grad else args.steps * (Nt - 2)) / elapsed,
-        "unit": "gradients/s" if grad else "rows/s",
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c128/f64",
-        "data": (f"synthetic GRAPE controls U(2,10) seed {c['seed']}; psi_init = "
-                 + (f"|1..1> evolved {args.c5_warm} steps at U=2.5 on the device (untimed, {warm_s:.0f} s; "
-                    f"max bond {int(ini.bond_dims().max())})" if c5 else "saturated chi=256 warm state")),
-        "config": {"workload": (f"config 4 chain, getAnalyticGradient over N_t={Nt} (T=4)" if grad else
-                                f"config {5 if c5 else 4} chain, getHessian over a T slice N_t={Nt} "
-                                f"({Nt - 2} rows, {row_steps} row-steps)"),
-                   "engine": "HBM-resident (hbm.hip)"},
-        "sweep_steps_per_sec": sweep / elapsed,
-        "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(st_traj["ms"] / max(1, st_traj["launches"]), 1e-9),
-        "mfma_gemm": {"kernel": "k_gemm (v_mfma_f64_16x16x4f64)", "launches_per_step": gm["launches"] / args.steps,
-                      "avg_launch_ms": gemm_ms, "share_of_time": gm["ms"] / (1e3 * elapsed),
-                      "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,
-                      "achieved_gbs": gm["alg_bytes"] / max(gm["ms"], 1e-9) / 1e6},
-        "roofline": roofline_block("hbm::k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
-                                   gm["alg_flops"] / max(1, gm["launches"]), args.profile_tag + ("c5" if c5 else "c4"),
-                                   limiter="the per-sector Hermitian eigensolver (k_heev_*: one CU per block, "
-                                           "latency-bound), not the MFMA contraction"),
-    }
-    print(json.dumps(res), flush=True)
+    if rank == 0:
+        tag = f"{args.profile_tag}{'c5' if c5 else 'c4'}{'g' if grad else ''}n{Nt}"
+        par = (f"one getHessian per step, rows zig-zag over {world} GPU(s), RCCL reduce to rank 0" if strong
+               else f"{world} GPU(s), one {'gradient' if grad else 'getHessian'} (own control) per GPU")
+        res = {
+            "metric": ("getAnalyticGradient/sec (psi || xi + divT)" if grad else "Hessian-rows/sec (getHessian)")
+                      + (", config 5 chain L=50 Npart=50 d=8 chi=512 tstep=0.01" if c5 else
+                         ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005"),
+            "value": (args.steps * KM * world if grad else args.steps * (Nt - 2) * reps) / elapsed,
+            "unit": "gradients/s" if grad else "rows/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+            "dtype": "c128/f64",
+            "data": ((f"synthetic GROUP coefficients U(-2,2) (M={M}, chopped sine, u0 adiabatic 2->10), "
+                      if M else "synthetic GRAPE controls U(2,10), ") + f"seed {c['seed']}, a fresh draw per step; "
+                     + "psi_init = " + (f"|1..1> evolved {args.c5_warm} steps at U=2.5 on the device (untimed, "
+                                        f"{warm_s:.0f} s; max bond {int(ini.bond_dims().max())})" if c5 else
+                                        "saturated chi=256 warm state")),
+            "config": {"workload": (f"config 4 chain, getAnalyticGradient over N_t={Nt} (T=4)" if grad else
+                                    f"config {5 if c5 else 4} chain, getHessian"
+                                    + (f" GROUP M={M} (convertControl, regularisation gamma={gamma}, "
+                                       f"convertHessian on the device)" if M else " GRAPE")
+                                    + f" over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)"),
+                       "engine": "HBM-resident (hbm.hip)", "parallelism": par},
+            "sweep_steps_per_sec": sweep / elapsed,
+            "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(st_traj["ms"] / max(1, st_traj["launches"]), 1e-9),
+            "mfma_gemm": {"kernel": "k_gemm (v_mfma_f64_16x16x4f64)", "launches_per_step": gm["launches"] / args.steps,
+                          "avg_launch_ms": gemm_ms, "share_of_time": gm["ms"] / (1e3 * elapsed),
+                          "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,
+                          "achieved_gbs": gm["alg_bytes"] / max(gm["ms"], 1e-9) / 1e6},
+            "roofline": roofline_block("hbm::k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
+                                       gm["alg_flops"] / max(1, gm["launches"]), tag, bound="latency",
+                                       limiter="the per-sector Hermitian eigensolver (k_heev_*) sets the step time; "
+                                               "k_gemm launches are small (tasks of m, n ~ 16-60) and latency-bound"),
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def measured_traffic(kernel, tag="r01"):

@@ -172,3 +172,33 @@ def test_c4_s32_gradient_multi(c4):
         eng.propagate(U[k], 3)
         assert np.array_equal(dm[k], eng.div_t()) and Fm[k] == eng.overlap_factor(), k
     eng.close()
+
+
+def test_c4_s32_row_shards_sum_bitwise(c4):
+    """config 4's row sharding on the HBM engine (bench.py --workload c4rows
+    --mode strong): each shard is its own context (own trajectories, as one
+    rank per GPU), rows dealt zig-zag over 3 shards; the shards' partial
+    Hessians sum to the unsharded getHessian bit for bit, and that equals the
+    oracle's (north_star tolerance)."""
+    from optimalcontrolmps_amd.native import Engine
+    from optimalcontrolmps_amd.sharding import zigzag_rows
+    u = c4["s32/u"]
+    Nt = len(u)
+    tgt, ini = _mps(c4["s32/tgt_dims"], c4["s32/tgt_data"]), _mps(c4["s32/init_dims"], c4["s32/init_data"])
+
+    def ctx():
+        e = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+        e.set_states(tgt, ini)
+        return e
+    e0 = ctx()
+    Hfull, d0, F0 = e0.hessian(u)
+    e0.close()
+    parts = []
+    for r in range(3):
+        e = ctx()
+        H, d, F = e.hessian(u, zigzag_rows(Nt - 2, r, 3))
+        assert np.array_equal(d, d0) and F == F0
+        parts.append(H)
+        e.close()
+    assert np.array_equal(parts[0] + parts[1] + parts[2], Hfull)
+    assert np.abs(Hfull - c4["s32/H"]).max() <= 1e-6 * np.abs(c4["s32/H"]).max()
