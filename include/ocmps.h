@@ -103,6 +103,16 @@ int ocg_step_batch(ocg_ctx* ctx, int n, const int* dims, const double* const* da
  * facade's InitializeState runs a tau schedule over this. */
 int ocg_imag_steps(ocg_ctx* ctx, const int* dims, const double* data, double U, double tau, int nsteps,
                    int* out_dims, double* out_data, size_t out_cap, size_t* out_nelem);
+/* InitializeState's ground state (include/InitializeState.hpp:18-117) in one
+ * call with the state resident on the device: for each tau of taus[0..ntau),
+ * imaginary-time steps (as ocg_imag_steps) in blocks of `block` until
+ * 1 - |<state before the block|state after>| < tol or max_steps per stage; one
+ * device overlap per block, no host round trip.  Returns the final state;
+ * *steps_done (optional) = total steps taken.  Real-time gates and device
+ * trajectories are left as they were. */
+int ocg_ground_state(ocg_ctx* ctx, const int* dims, const double* data, double U, int ntau, const double* taus,
+                     int block, double tol, int max_steps, int* out_dims, double* out_data, size_t out_cap,
+                     size_t* out_nelem, int* steps_done);
 /* overlapC(x, y) = <x|y> (with_dH = 0) or overlapC(x, propDeriv, y) = <x|dH|y>
  * (with_dH = 1) (src/OptimalControl.cpp:242, :412); out = {re, im} */
 int ocg_overlap(ocg_ctx* ctx, const int* dims_x, const double* x, const int* dims_y, const double* y,

@@ -2370,3 +2370,48 @@ int hbm_denmat_decomp(hbm_engine* h, int nm, const int* rows, const int* cols, c
     for (int i = 0; i < nm; ++i) kept[i] = k[i];
   });
 }
+
+// InitializeState on the device (ocg_ground_state): the tau schedule of
+// imaginary-time steps with the state resident in one chain; per block of
+// `block` steps one overlap with the block's starting state (a heap slot),
+// 1 - |<prev|new>| < tol ends a stage.  Only the final state is downloaded.
+// gf / gb[t]: the exp(-tau_t h) gate tables (layout glo / gsz / goff as the
+// real-time ones); the real-time tables (dt0) are restored afterwards.
+int hbm_ground_state(hbm_engine* h, const int* dims, const double* data, double U, int ntau, const double* taus,
+                     const std::vector<std::vector<double>>& gf, const std::vector<std::vector<double>>& gb,
+                     const int* glo, const int* gsz, const int* goff, int gtotal, double dt0,
+                     const std::vector<double>& gf0, const std::vector<double>& gb0, int block, double tol,
+                     int max_steps, int* out_dims, double* out_data, size_t cap, size_t* nelem, int* steps_done) {
+  int done = 0;
+  const int rc = guard(h, [&] {
+    hbm::Engine& E = *h->E;
+    E.set_caps(widest_of(E, dims));
+    E.reserve_states(size_t(h->xih_base() + h->N + 2));
+    const int prev = h->xih_base() + h->N;  // scratch slot after the trajectories
+    E.upload_state(E.states[prev], dims, data);
+    E.reserve_chains(std::max(E.nchain_cap, 1), false);
+    std::vector<Chain*> cs{E.acquire(false)};
+    E.load_many(cs, {E.states[prev].view()});
+    Timer t(h, 4);
+    for (int s = 0; s < ntau; ++s) {
+      E.dt = taus[s];
+      E.set_gates(gf[s], gb[s], glo, gsz, goff, gtotal);
+      E.gcst.imag = 1;
+      for (int d = 0; d < max_steps; d += block) {
+        E.store_many({&E.states[prev]}, cs);
+        for (int k = 0; k < block; ++k) E.step(cs, {U}, {U}, {1});
+        done += block;
+        const auto ov = E.overlaps({E.states[prev].view()}, {cs[0]->view()}, false);
+        if (1.0 - std::abs(ov[0]) < tol) break;
+      }
+    }
+    t.stop(done);
+    const size_t tot = E.download_view(cs[0]->view(), out_dims, out_data, cap);
+    if (nelem) *nelem = tot;
+    E.release(cs[0]);
+    if (tot > cap) throw hbm::Error(2, "output buffer too small");
+  });
+  const int rc2 = hbm_swap_gates(h, 0, dt0, gf0, gb0, glo, gsz, goff, gtotal);
+  if (steps_done) *steps_done = done;
+  return rc ? rc : rc2;
+}

@@ -61,3 +61,9 @@ int hbm_N(const hbm_engine* h);
 // denmatDecomp (Fromleft) of nm independent dense blocks (ocg_denmat_decomp)
 int hbm_denmat_decomp(hbm_engine* h, int nm, const int* rows, const int* cols, const double* const* M, double cutoff,
                       int maxm, int* kept, double* const* w, double* const* X, double* const* Y);
+// InitializeState's imaginary-time schedule with the state resident on the device (ocg_ground_state)
+int hbm_ground_state(hbm_engine* h, const int* dims, const double* data, double U, int ntau, const double* taus,
+                     const std::vector<std::vector<double>>& gf, const std::vector<std::vector<double>>& gb,
+                     const int* glo, const int* gsz, const int* goff, int gtotal, double dt0,
+                     const std::vector<double>& gf0, const std::vector<double>& gb0, int block, double tol,
+                     int max_steps, int* out_dims, double* out_data, size_t cap, size_t* nelem, int* steps_done);

@@ -788,6 +788,73 @@ int ocg_imag_steps(ocg_ctx* c, const int* dims, const double* data, double U, do
   return rc ? rc : rc2;
 }
 
+static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::vector<int>& ys, int with_dH,
+                           std::vector<zc>& out);
+
+// InitializeState's whole tau schedule with the state resident on the device:
+// per stage blocks of `block` imaginary-time steps until 1 - |<prev|new>| < tol
+// (or max_steps), one device overlap per block, no host round trip.
+int ocg_ground_state(ocg_ctx* c, const int* dims, const double* data, double U, int ntau, const double* taus,
+                     int block, double tol, int max_steps, int* out_dims, double* out_data, size_t out_cap,
+                     size_t* out_nelem, int* steps_done) {
+  if (!c || !dims || !data || !out_dims || !out_data || ntau < 0 || (ntau > 0 && !taus) || block < 1 ||
+      max_steps < 0)
+    return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  for (int s = 0; s < ntau; ++s)
+    if (!(taus[s] > 0)) return fail(c, OCG_EINVAL, "tau must be > 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  const double dt0 = c->P.dt;
+  if (c->hbm) {
+    OcgParams G{};
+    G.p = c->P.p;
+    G.imag = 1;
+    std::vector<std::vector<double>> gf(ntau), gb(ntau);
+    for (int s = 0; s < ntau; ++s) {
+      G.dt = taus[s];
+      ocg_host::gate_tables(G, c->J, gf[s], gb[s]);
+    }
+    G.dt = dt0;
+    G.imag = 0;
+    std::vector<double> gf0, gb0;
+    ocg_host::gate_tables(G, c->J, gf0, gb0);
+    return hb(c, hbm_ground_state(c->hbm, dims, data, U, ntau, taus, gf, gb, G.glo, G.gsz, G.goff, G.gtotal, dt0,
+                                  gf0, gb0, block, tol, max_steps, out_dims, out_data, out_cap, out_nelem, steps_done));
+  }
+  // LDS engine: the state in scratch slot 0, the block's starting state copied to slot 1
+  const OcgParams& P = c->P;
+  const int a = c->slot_tmp(0), b = c->slot_tmp(1);
+  if (int rc = upload_mps(c, a, dims, data)) return rc;
+  const std::vector<double> u(size_t(block) + 1, U);
+  int done = 0, rc = 0;
+  for (int s = 0; s < ntau && !rc; ++s) {
+    c->P.dt = taus[s];
+    c->P.imag = 1;
+    if ((rc = upload_gates(c))) break;
+    for (int d = 0; d < max_steps; d += block) {
+      hipError_t e = hipMemcpyAsync(SLOT_D(c->pool, P, b), SLOT_D(c->pool, P, a), sizeof(int) * P.nsq,
+                                    hipMemcpyDeviceToDevice, c->stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(SLOT_X(c->pool, P, b), SLOT_X(c->pool, P, a), sizeof(zc) * P.cap, hipMemcpyDeviceToDevice,
+                           c->stream);
+      if (e != hipSuccess) {
+        rc = fail(c, OCG_EHIP, std::string("slot copy: ") + hipGetErrorString(e));
+        break;
+      }
+      if ((rc = launch_steps(c, a, u.data(), block, 1))) break;
+      done += block;
+      std::vector<zc> ov;
+      if ((rc = launch_overlaps(c, {b}, {a}, 0, ov))) break;
+      if (1.0 - std::hypot(ov[0].x, ov[0].y) < tol) break;
+    }
+  }
+  c->P.dt = dt0;
+  c->P.imag = 0;
+  const int rc2 = upload_gates(c);
+  if (steps_done) *steps_done = done;
+  if (rc || rc2) return rc ? rc : rc2;
+  return download_mps(c, a, out_dims, out_data, out_cap, out_nelem);
+}
+
 int ocg_step_batch(ocg_ctx* c, int n, const int* dims, const double* const* data, const double* u_from,
                    const double* u_to, int forward, int* out_dims, double* const* out_data, const size_t* out_cap,
                    size_t* out_nelem) {

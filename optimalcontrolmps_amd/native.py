@@ -97,6 +97,8 @@ SIGNATURES = [
     ("ocg_step", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_steps", C.c_int, [C.c_void_p, ip, dp, dp, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_imag_steps", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
+    ("ocg_ground_state", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_int, dp, C.c_int, C.c_double, C.c_int, ip, dp,
+                                   C.c_size_t, szp, ip]),
     ("ocg_step_batch", C.c_int, [C.c_void_p, C.c_int, ip, C.POINTER(dp), dp, dp, C.c_int, ip, C.POINTER(dp), szp,
                                  szp]),
     ("ocg_overlap", C.c_int, [C.c_void_p, ip, dp, ip, dp, C.c_int, dp]),
@@ -234,6 +236,19 @@ class Engine:
         self._chk(lib().ocg_imag_steps(self.h, pd, pr, float(U), float(tau), int(nsteps), fd.ctypes.data_as(ip),
                                        d.ctypes.data_as(dp), self.cap, C.byref(n)), "ocg_imag_steps")
         return self._wrap(fd, d, n)
+
+    def ground_state(self, m: MPS, U, taus, block=25, tol=1e-13, max_steps=8000):
+        """InitializeState's tau schedule on the device in one call (ocg_ground_state):
+        returns (state, steps taken)"""
+        fd, d, n = self._out()
+        _, pd = _i(m.dims)
+        raw, pr = _d(m.raw())
+        tt, pt = _d(np.asarray(taus, np.float64))
+        steps = C.c_int(0)
+        self._chk(lib().ocg_ground_state(self.h, pd, pr, float(U), len(tt), pt, int(block), float(tol), int(max_steps),
+                                         fd.ctypes.data_as(ip), d.ctypes.data_as(dp), self.cap, C.byref(n),
+                                         C.byref(steps)), "ocg_ground_state")
+        return self._wrap(fd, d, n), steps.value
 
     def step_batch(self, states, u_from, u_to, forward=True):
         """one step of every state (own controls each) in a single launch"""

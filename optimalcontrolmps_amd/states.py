@@ -54,17 +54,9 @@ def ground_state(engine, U: float, taus=GS_TAUS, block: int = 25, tol: float = 1
                  max_steps: int = 8000, psi: MPS = None) -> MPS:
     """InitializeState(sites, Npart, J, U) (include/InitializeState.hpp:18-117) on
     the device: imaginary-time evolution exp(-tau H) of the product state
-    |0..0 1..1> (the reference's DMRG starting guess) through ocg_imag_steps,
-    in blocks of `block` steps per tau until 1 - |<prev|new>| < tol."""
+    |0..0 1..1> (the reference's DMRG starting guess), per tau in blocks of
+    `block` steps until 1 - |<prev|new>| < tol, the whole schedule in one
+    ocg_ground_state call (the state stays on the device)."""
     if psi is None:
         psi = product_state(engine.L, engine.p, engine.Q)
-    for tau in taus:
-        done = 0
-        while done < max_steps:
-            new = engine.imag_steps(psi, U, tau, block)
-            d = 1.0 - abs(engine.overlap(psi, new))
-            psi = new
-            done += block
-            if d < tol:
-                break
-    return psi
+    return engine.ground_state(psi, U, taus, block, tol, max_steps)[0]

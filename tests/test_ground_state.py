@@ -24,9 +24,9 @@ def infidelity(dims, data, U):
     return 1.0 - abs(np.vdot(gs, v)) ** 2 / (np.vdot(v, v).real * np.vdot(gs, gs).real)
 
 
-@pytest.mark.parametrize("U,engine", [(2.5, "lds"), (50.0, "lds"), (50.0, "hbm")])
+@pytest.mark.parametrize("U,engine", [(2.5, "lds"), (50.0, "lds"), (2.5, "hbm"), (50.0, "hbm")])
 def test_ground_state_vs_ed(U, engine):
-    """(the HBM engine runs U = 50 only: U = 2.5 needs ~5k host-driven steps)"""
+    """the whole tau schedule in one ocg_ground_state call (state resident on the device)"""
     from optimalcontrolmps_amd.native import Engine
     from optimalcontrolmps_amd.states import ground_state
     eng = Engine(L, p, N, J, 0.01, 1e-9, 80, engine=engine)
@@ -67,3 +67,41 @@ def test_facade_initialize_state():
     for U, k in ((2.5, "U2.5"), (50.0, "U50")):
         x = np.asarray(r[k + "_data"])
         assert infidelity(r[k + "_dims"], x[0::2] + 1j * x[1::2], U) < TOL[U]
+
+
+@pytest.mark.parametrize("U", [2.0, 6.0])
+def test_ground_state_L10_vs_lanczos(U):
+    """L = 10 (p = 5, N = 10: 72,403 sector states, beyond the dense ED of the
+    L = 5 tests): device ground state (ocg_ground_state, InitializeState's
+    defaults maxBondDim 200 / threshold 1e-9, taus 0.05 -> 0.002) against scipy
+    Lanczos on the sector Hamiltonian (tests/golden/gs_L10.npz, made by
+    tests/golden/make_gs_fixtures.py): energy, <n_i> and the hopping
+    correlations <a^dag_i a_{i+1}> (whose sum with the on-site term reproduces
+    E0 exactly).  Tolerances: the tau = 0.002 Trotter fixed point is off the
+    exact ground state at O(tau^2)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_gs_fixtures as G
+    from optimalcontrolmps_amd.native import Engine
+    from optimalcontrolmps_amd.states import product_state
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "gs_L10.npz"), allow_pickle=False)
+    key = f"U{U:g}"
+    Lx, px, Nx = G.L, G.P, G.NPART
+    eng = Engine(Lx, px, Nx, G.J, 0.01, 1e-9, 200)
+    psi, steps = eng.ground_state(product_state(Lx, px, Nx), U, (0.05, 0.01, 0.002), block=25, tol=1e-11,
+                                  max_steps=20000)
+    full = ed.full_from_mps(psi.dims, psi.data, Lx, px, Nx)
+    idx, dg = G.sector(Lx, px, Nx)
+    v = full[idx]
+    assert abs(np.vdot(full, full).real - np.vdot(v, v).real) < 1e-12   # particle number exact
+    v = v / np.linalg.norm(v)
+    n, hop = G.observables_sector(v, dg, idx, Lx, px)
+    E = -G.J * 2 * hop.sum() + 0.5 * U * ((dg * (dg - 1)) * np.abs(v) ** 2).sum()
+    E0 = float(z[key + "/E0"])
+    print(f"L=10 U={U}: {steps} steps, E - E0 = {E - E0:.3e}, max|dn| = {np.abs(n - z[key + '/n']).max():.3e}, "
+          f"max|dhop| = {np.abs(hop - z[key + '/hop']).max():.3e}, bonds {list(psi.bond_dims())}")
+    assert E >= E0 - 1e-9                      # variational
+    assert E - E0 < 2e-4 * abs(E0)
+    assert np.abs(n - z[key + "/n"]).max() < 2e-3
+    assert np.abs(hop - z[key + "/hop"]).max() < 2e-3
