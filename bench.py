@@ -58,7 +58,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=8)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="largest CPU-baseline thread count (0: all available)")
     ap.add_argument("--mode", choices=["weak", "strong"], default=None,
                     help="weak: every rank its own getHessian; strong: one getHessian's rows over the ranks "
                          "(default: weak for config 1, strong for c4rows / c5rows)")
@@ -521,24 +521,44 @@ def measured_traffic(kernel, tag="r01"):
         return None
 
 
+def cpu_threads_available():
+    """host threads this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS when set (the GPU box exports its CPU share, 16 per GPU)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(ini, tgt, u, threads):
     """The CPU restatement (oracle/, 'port' — ITensor cannot be built here) timed
-    on host cores: full getHessian with a row worker pool like
-    calcHessian_parallel (src/OptimalControl.cpp:281-338)."""
+    on host cores like main/TestRuntimes.cpp:25-229: one full getHessian per
+    thread count 1, 2, 4, 8, ... up to the threads available (row worker pool of
+    calcHessian_parallel, src/OptimalControl.cpp:281-338, psi || xi on two
+    threads); value = the best rate, cores = the threads it used."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     L, p, Q, J, dt = CFG["L"], CFG["p"], CFG["npart"], CFG["J"], CFG["tstep"]
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    avail = cpu_threads_available()
+    cap = max(1, min(threads, avail)) if threads else avail
+    counts = sorted({t for t in (1, 2, 4, 8, 16, 32) if t <= cap} | {cap})
     st = O.Stepper(L, p, Q, J, dt, CFG["cutoff"], CFG["maxm"])
     oc = O.OC(st, O.MPS(L, p, Q, tgt.dims, tgt.data), O.MPS(L, p, Q, ini.dims, ini.data), len(u), 0.0)
-    reps, total = 0, 0.0
-    while total < 10.0 and reps < 8:
-        total += oc.time_hessian(u, threads)
-        reps += 1
     Nt = len(u)
-    return {"value": reps * (Nt - 2) / total, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} full getHessian calls (config 1, 199 rows each) on the C++ CPU restatement "
-                      f"(oracle/, not ITensor), {threads} row-worker threads, {total:.1f} s"}
+    sweep, total = {}, 0.0
+    for t in counts:
+        dt_s = oc.time_hessian(u, t)
+        total += dt_s
+        sweep[str(t)] = (Nt - 2) / dt_s
+    best = max(counts, key=lambda t: sweep[str(t)])
+    return {"value": sweep[str(best)], "unit": "rows/s", "cores": best, "kind": "port",
+            "threads_sweep_rows_per_sec": sweep, "host_threads_available": avail, "nproc": os.cpu_count(),
+            "sample": f"one full getHessian (config 1, {Nt - 2} rows) per thread count {counts} on the C++ CPU "
+                      f"restatement (oracle/, not ITensor; main/TestRuntimes.cpp's thread sweep), {total:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -21,6 +21,8 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <cstdio>
@@ -29,6 +31,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hbm.hpp"
@@ -254,9 +257,6 @@ struct Engine {
     thost.pinned = true;
     HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
-    HCK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
-    HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     md = md_in;
     mdz = mdz_in;
     gate_i1 = gates;
@@ -772,6 +772,11 @@ struct Engine {
         for (int i = 0; i < np; ++i) ++eig_hist[std::min(R.probs[i].n / 16, 33)];
       std::stable_sort(big.begin(), big.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
       if (!big.empty()) {  // on the side stream, after everything st has queued (incl. this upload)
+        if (!st2) {  // created on first use: every stream takes a hardware queue (GPU_MAX_HW_QUEUES)
+          HCK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+          HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+          HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+        }
         const int* dbig = upload(big);
         HCK(hipEventRecord(ev_fork, st));
         HCK(hipStreamWaitEvent(st2, ev_fork, 0));
@@ -1680,6 +1685,13 @@ using hbm::View;
 
 struct hbm_engine {
   std::unique_ptr<hbm::Engine> E;
+  // worker engines of the pipelined getHessian (own stream, arenas, chains; they
+  // read and write E's state heap) and what they are built from
+  std::unique_ptr<hbm::Engine> W[2];
+  std::vector<int> md, mdz, gates;
+  std::vector<double> gf, gb;
+  int glo[24] = {0}, gsz[24] = {0}, goff[24] = {0}, gtotal = 0;
+  long gates_version = 0, w_version[2] = {-1, -1};
   std::string err;
   int N = 0;
   bool have_states = false, have_psi = false, have_xi = false, have_xih = false;
@@ -1748,6 +1760,13 @@ int hbm_create(int device, int L, int p, int npart, double J, double tstep, doub
                const std::vector<int>& gates, hbm_engine** out, std::string& err) {
   auto* h = new hbm_engine;
   h->E.reset(new hbm::Engine(device, L, p, npart, J, tstep, cutoff, maxm));
+  h->md = md;
+  h->mdz = mdz;
+  h->gates = gates;
+  h->gf = gf;
+  h->gb = gb;
+  for (int D = 0; D < 24; ++D) { h->glo[D] = glo[D]; h->gsz[D] = gsz[D]; h->goff[D] = goff[D]; }
+  h->gtotal = gtotal;
   try {
     HCK(hipSetDevice(device));
     h->E->init(md, mdz, gf, gb, glo, gsz, goff, gtotal, gates);
@@ -1777,6 +1796,9 @@ int hbm_set_tstep(hbm_engine* h, double tstep, const std::vector<double>& gf, co
     h->E->dt = tstep;
     h->E->set_gates(gf, gb, glo, gsz, goff, gtotal);
     h->have_psi = h->have_xi = h->have_xih = false;
+    h->gf = gf;
+    h->gb = gb;
+    ++h->gates_version;
   });
 }
 
@@ -2414,4 +2436,289 @@ int hbm_ground_state(hbm_engine* h, const int* dims, const double* data, double 
   const int rc2 = hbm_swap_gates(h, 0, dt0, gf0, gb0, glo, gsz, goff, gtotal);
   if (steps_done) *steps_done = done;
   return rc ? rc : rc2;
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined getHessian (calcHessian_*, src/OptimalControl.cpp:281-372): the
+// psi chain, the rows, the dH applications and the xi chain run concurrently
+// instead of one after the other, so a Hessian slice costs about one
+// trajectory's latency instead of two trajectories plus the longest row.
+//   main thread, engine E : one lockstep batch of the psi chain (t -> t+1) and
+//                           every row that has joined (row i at its own time:
+//                           per-chain controls), each row state stored for
+//                           its overlap (RS slots); publishes psi_t
+//   thread H, worker W[0] : psiH_i = exactApplyMPO(dH, psi_i) and normiH as
+//                           psi_i appears (:256-257); publishes the row
+//   thread X, worker W[1] : xi backward from the target (:392-407), then
+//                           xiH_t = exactApplyMPO(dH, xi_t) (:300-303)
+// then one batched launch sequence of every overlap: divT (:409-419), F (:242)
+// and <xiH_j|psiH_i(j)> (:261, :272).  Same steps, decompositions, dH
+// applications and overlaps as hbm_propagate + hbm_xi_dH + hbm_hessian_rows,
+// and every kernel is batch-independent, so the same numbers bit for bit.
+// Memory: the stored trajectories plus one state per (row, later time).
+// ---------------------------------------------------------------------------
+namespace {
+hbm::Engine& pipe_worker(hbm_engine* h, int k) {
+  hbm::Engine& E = *h->E;
+  auto& W = h->W[k];
+  if (W && (W->bcap != E.bcap || W->bcapw != E.bcapw)) W.reset();
+  if (!W) {
+    W.reset(new hbm::Engine(E.device, E.L, E.p, E.Q, E.J, E.dt, E.cutoff, E.maxm));
+    W->init(h->md, h->mdz, h->gf, h->gb, h->glo, h->gsz, h->goff, h->gtotal, h->gates);
+    W->set_caps(E.widest);
+    if (W->bcap != E.bcap || W->bcapw != E.bcapw || W->state_cap != E.state_cap)
+      throw hbm::Error(3, "internal: worker engine capacities differ");
+    h->w_version[k] = h->gates_version;
+  }
+  if (h->w_version[k] != h->gates_version) {
+    W->set_gates(h->gf, h->gb, h->glo, h->gsz, h->goff, h->gtotal);
+    h->w_version[k] = h->gates_version;
+  }
+  W->dt = E.dt;
+  W->gcst.imag = 0;
+  return *W;
+}
+// first slot of the row states and the slots the pipeline needs in total
+int pipe_psih_base(const hbm_engine* h, int N) { return 4 + 3 * N + 2; }
+}  // namespace
+
+double hbm_pipe_bytes(const hbm_engine* h, int N, const int* rows, int nrows) {
+  double slots = pipe_psih_base(h, N) + N;
+  for (int r = 0; r < nrows; ++r) slots += std::max(0, N - 2 - rows[r]);
+  return 16.0 * double(h->E->state_cap) * slots;
+}
+
+int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                     double* F) {
+  return guard(h, [&] {
+    if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
+    hbm::Engine& E = *h->E;
+    std::vector<int> rs(rows, rows + nrows);
+    std::sort(rs.begin(), rs.end());
+    hbm_prepare_N(h, N);
+    h->have_psi = h->have_xi = h->have_xih = false;  // the trajectory slots are overwritten
+    const int psih0 = pipe_psih_base(h, N);
+    std::vector<int> rsoff(nrows + 1);
+    rsoff[0] = psih0 + N;
+    for (int k = 0; k < nrows; ++k) rsoff[k + 1] = rsoff[k] + (N - 2 - rs[k]);
+    E.reserve_states(size_t(rsoff[nrows]));
+    hbm::Engine& WH = pipe_worker(h, 0);
+    hbm::Engine& WX = pipe_worker(h, 1);
+    const int dev = E.device;
+    const int B = hbm_batch(h, N);
+    Timer tall(h, 5);
+    std::atomic<int> psi_ready(-1), psih_ready(0), abort_(0);
+    std::vector<double> nrm(nrows, 0.0);
+    auto wait_for = [&](const std::atomic<int>& a, int v) {
+      while (a.load(std::memory_order_acquire) < v) {
+        if (abort_.load()) throw hbm::Error(3, "pipelined getHessian: another stage failed");
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    };
+    std::exception_ptr ex[3];
+    // X: xi_t backward from the target, then xiH_t for every t
+    std::thread tx([&] {
+      try {
+        HCK(hipSetDevice(dev));
+        hbm::Engine& W = WX;
+        W.reserve_chains(std::max(W.nchain_cap, B), false);
+        {
+          std::vector<Chain*> c1{W.acquire(false)};
+          W.load_many(c1, {E.states[1].view()});
+          W.store_many({&E.states[h->xi_base() + N - 1]}, c1);
+          for (int s = 0; s + 1 < N && !abort_.load(); ++s) {
+            W.step(c1, {u[N - 1 - s]}, {u[N - 2 - s]}, {0});
+            W.store_many({&E.states[h->xi_base() + N - 2 - s]}, c1);
+          }
+          W.sync();
+          W.release(c1[0]);
+        }
+        for (int t0 = 0; t0 < N && !abort_.load(); t0 += B) {
+          const int nb = std::min(B, N - t0);
+          std::vector<View> in;
+          std::vector<Chain*> out;
+          std::vector<State*> ss;
+          for (int i = 0; i < nb; ++i) {
+            in.push_back(E.states[h->xi_base() + t0 + i].view());
+            out.push_back(W.acquire(false));
+            ss.push_back(&E.states[h->xih_base() + t0 + i]);
+          }
+          W.apply_dH(in, out);
+          W.store_many(ss, out);
+          W.sync();
+          for (auto* c : out) W.release(c);
+        }
+      } catch (...) {
+        ex[1] = std::current_exception();
+        abort_.store(1);
+        (void)hipStreamSynchronize(WX.st);
+        WX.release_all();
+      }
+    });
+    // H: psiH_i = dH psi_i and its norm as psi_i appears, up to 8 rows per batch
+    std::thread th([&] {
+      try {
+        HCK(hipSetDevice(dev));
+        hbm::Engine& W = WH;
+        constexpr int kJoin = 8;
+        W.reserve_chains(std::max(W.nchain_cap, kJoin), false);
+        for (int next = 0; next < nrows;) {
+          wait_for(psi_ready, rs[next]);
+          const int avail = psi_ready.load(std::memory_order_acquire);
+          int end = next;
+          while (end < nrows && rs[end] <= avail && end - next < kJoin) ++end;
+          std::vector<View> in;
+          std::vector<Chain*> out;
+          std::vector<State*> ss;
+          for (int k = next; k < end; ++k) {
+            in.push_back(E.states[h->psi_base() + rs[k]].view());
+            out.push_back(W.acquire(false));
+            ss.push_back(&E.states[psih0 + k]);
+          }
+          W.apply_dH(in, out);
+          std::vector<View> vs;
+          for (auto* c : out) vs.push_back(c->view());
+          const std::vector<double> n2 = W.site_norm2(vs, 1);
+          for (int k = next; k < end; ++k) nrm[k] = std::sqrt(std::max(0.0, n2[k - next]));
+          W.store_many(ss, out);
+          W.sync();
+          for (auto* c : out) W.release(c);
+          psih_ready.store(end, std::memory_order_release);
+          next = end;
+        }
+      } catch (...) {
+        ex[2] = std::current_exception();
+        abort_.store(1);
+        (void)hipStreamSynchronize(WH.st);
+        WH.release_all();
+      }
+    });
+    // A (this thread): the psi chain and the rows in one lockstep batch
+    try {
+      E.reserve_chains(std::max(E.nchain_cap, nrows + 1), false);
+      struct RowRun {
+        Chain* c;
+        int k, t;  // row index in rs, time of the chain's state
+      };
+      Chain* psi = E.acquire(false);
+      {
+        std::vector<Chain*> p1{psi};
+        E.load_many(p1, {E.states[0].view()});
+        E.store_many({&E.states[h->psi_base()]}, p1);
+        E.sync();
+      }
+      psi_ready.store(0, std::memory_order_release);
+      std::vector<RowRun> act;
+      int joined = 0, tpsi = 0;
+      while (tpsi < N - 1 || !act.empty() || joined < nrows) {
+        if (abort_.load()) throw hbm::Error(3, "pipelined getHessian: another stage failed");
+        const int pr = psih_ready.load(std::memory_order_acquire);
+        if (joined < pr) {  // rows whose psiH is ready join the batch (row N-2: diagonal only)
+          std::vector<Chain*> jc;
+          std::vector<View> jv;
+          std::vector<int> jk;
+          for (int k = joined; k < pr; ++k) {
+            if (rs[k] >= N - 2) continue;
+            jc.push_back(E.acquire(false));
+            jv.push_back(E.states[psih0 + k].view());
+            jk.push_back(k);
+          }
+          E.load_many(jc, jv);
+          for (size_t m = 0; m < jk.size(); ++m) act.push_back({jc[m], jk[m], rs[jk[m]]});
+          joined = pr;
+        }
+        std::vector<Chain*> cs;
+        std::vector<double> uf, ut;
+        std::vector<int> fw;
+        std::vector<State*> ss;
+        const bool with_psi = tpsi < N - 1;
+        if (with_psi) {
+          cs.push_back(psi);
+          uf.push_back(u[tpsi]);
+          ut.push_back(u[tpsi + 1]);
+          fw.push_back(1);
+          ss.push_back(&E.states[h->psi_base() + tpsi + 1]);
+        }
+        for (auto& r : act) {  // timeStepper.step(psiH, u[j-1], u[j]) (:269), j = t + 1
+          cs.push_back(r.c);
+          uf.push_back(u[r.t]);
+          ut.push_back(u[r.t + 1]);
+          fw.push_back(1);
+          ss.push_back(&E.states[rsoff[r.k] + (r.t - rs[r.k])]);
+        }
+        if (cs.empty()) {  // everything joined so far is done: wait for the next row
+          wait_for(psih_ready, joined + 1);
+          continue;
+        }
+        E.step(cs, uf, ut, fw);
+        E.store_many(ss, cs);
+        E.sync();
+        if (with_psi) psi_ready.store(++tpsi, std::memory_order_release);
+        for (auto& r : act) ++r.t;
+        std::vector<RowRun> keep;
+        for (auto& r : act) {
+          if (r.t >= N - 2) E.release(r.c);
+          else keep.push_back(r);
+        }
+        act.swap(keep);
+      }
+      E.release(psi);
+    } catch (...) {
+      ex[0] = std::current_exception();
+      abort_.store(1);
+    }
+    tx.join();
+    th.join();
+    for (auto& e : ex)
+      if (e) std::rethrow_exception(e);
+    for (hbm::Engine* W : {&WH, &WX}) {  // the workers' GEMM statistics belong to this context
+      W->sync();
+      E.gemm_ms += W->gemm_ms;
+      E.gemm_flops += W->gemm_flops;
+      E.gemm_bytes += W->gemm_bytes;
+      E.gemm_launches += W->gemm_launches;
+      W->gemm_ms = W->gemm_flops = W->gemm_bytes = 0;
+      W->gemm_launches = 0;
+    }
+    h->have_psi = h->have_xi = h->have_xih = true;
+    // overlaps: F, divT, then every <xiH_j|psiH_i(j)> in one batch
+    const std::complex<double> Fc =
+        E.overlaps({E.states[h->psi_base() + N - 1].view()}, {E.states[1].view()}, false)[0];
+    F[0] = Fc.real();
+    F[1] = Fc.imag();
+    std::vector<View> xs, ys;
+    for (int t = 0; t < N; ++t) {
+      xs.push_back(E.states[h->xi_base() + t].view());
+      ys.push_back(E.states[h->psi_base() + t].view());
+    }
+    const auto dvr = E.overlaps(xs, ys, true);
+    for (int t = 0; t < N; ++t) { divT[2 * t] = dvr[t].real(); divT[2 * t + 1] = dvr[t].imag(); }
+    auto dv = [&](int i) { return std::complex<double>(divT[2 * i], divT[2 * i + 1]); };
+    const std::complex<double> Fh(F[0], F[1]);
+    xs.clear();
+    ys.clear();
+    for (int k = 0; k < nrows; ++k) {
+      xs.push_back(E.states[h->xih_base() + rs[k]].view());
+      ys.push_back(E.states[psih0 + k].view());
+      for (int j = rs[k] + 1; j <= N - 2; ++j) {
+        xs.push_back(E.states[h->xih_base() + j].view());
+        ys.push_back(E.states[rsoff[k] + (j - rs[k] - 1)].view());
+      }
+    }
+    const auto ov = E.overlaps(xs, ys, false);
+    const double dt2 = E.dt * E.dt;
+    size_t e = 0;
+    for (int k = 0; k < nrows; ++k) {
+      const int i = rs[k];
+      H[size_t(i) * N + i] = dt2 * ((Fh * ov[e++]).real() - std::norm(dv(i)));  // (:259-264)
+      for (int j = i + 1; j <= N - 2; ++j) {                                     // (:266-278)
+        const double v1 = (Fh * ov[e++] * nrm[k]).real();
+        const double v2 = -(dv(i) * std::conj(dv(j))).real();
+        const double r = dt2 * (v1 + v2);
+        H[size_t(i) * N + j] = r;
+        H[size_t(j) * N + i] = r;
+      }
+    }
+    tall.stop(long(N - 1) * 2 + long(rsoff[nrows] - rsoff[0]));
+  });
 }

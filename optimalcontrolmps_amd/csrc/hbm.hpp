@@ -67,3 +67,10 @@ int hbm_ground_state(hbm_engine* h, const int* dims, const double* data, double 
                      const int* glo, const int* gsz, const int* goff, int gtotal, double dt0,
                      const std::vector<double>& gf0, const std::vector<double>& gb0, int block, double tol,
                      int max_steps, int* out_dims, double* out_data, size_t cap, size_t* nelem, int* steps_done);
+// getHessian's fidelity part with the psi chain + rows, the dH applications and
+// the xi chain pipelined on three engines (one stream each), row states stored
+// for one batched overlap pass; bit-identical to propagate + xi_dH + rows
+int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
+                     double* F);
+// heap bytes hbm_hessian_pipe needs (trajectories + psiH_i + row states)
+double hbm_pipe_bytes(const hbm_engine* h, int N, const int* rows, int nrows);

@@ -1255,6 +1255,23 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
       c->u_xi.clear();
       return hb(c, hbm_hessian_ckpt(c->hbm, u, N, rows, nrows, H, divT, F, K));
     }
+    // pipelined (psi + rows || dH || xi on three streams) when the row states fit
+    // half the free HBM and the trajectories of u are not already on the device
+    // (BH_nlp::eval_h after eval_grad_f reuses them); OCG_HBM_PIPE=0 turns it off
+    const char* pe = std::getenv("OCG_HBM_PIPE");
+    const int pipe_env = pe ? std::atoi(pe) : -1;
+    const bool reuse = hbm_have(c->hbm, 1) && hbm_have(c->hbm, 2) && same_u(c->u_psi, u, N) && same_u(c->u_xi, u, N);
+    if (pipe_env != 0 && !reuse && nrows > 0) {
+      size_t fr = 0, tot = 0;
+      HIPCHK(c, hipMemGetInfo(&fr, &tot));
+      if (hbm_pipe_bytes(c->hbm, N, rows, nrows) <= 0.5 * double(fr)) {
+        c->u_psi.clear();
+        c->u_xi.clear();
+        const int rc = hb(c, hbm_hessian_pipe(c->hbm, u, N, rows, nrows, H, divT, F));
+        if (!rc) note_u(c, u, N, 3);
+        return rc;
+      }
+    }
     return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
   }
   return hessian_fused(c, 1, u, N, rows, nrows, H, divT, F);

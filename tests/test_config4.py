@@ -202,3 +202,32 @@ def test_c4_s32_row_shards_sum_bitwise(c4):
         e.close()
     assert np.array_equal(parts[0] + parts[1] + parts[2], Hfull)
     assert np.abs(Hfull - c4["s32/H"]).max() <= 1e-6 * np.abs(c4["s32/H"]).max()
+
+
+def test_c4_s32_pipelined_equals_stored(c4, monkeypatch):
+    """the pipelined HBM getHessian (psi + rows || dH || xi on three engines,
+    hbm_hessian_pipe) equals the stored two-phase path (propagate + xi_dH +
+    rows, OCG_HBM_PIPE=0) bit for bit, for all rows and for a zig-zag shard,
+    and leaves the same device trajectories"""
+    from optimalcontrolmps_amd.native import Engine
+    from optimalcontrolmps_amd.sharding import zigzag_rows
+    u = c4["s32/u"]
+    Nt = len(u)
+    tgt, ini = _mps(c4["s32/tgt_dims"], c4["s32/tgt_data"]), _mps(c4["s32/init_dims"], c4["s32/init_data"])
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("OCG_HBM_PIPE", mode)
+        e = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+        e.set_states(tgt, ini)
+        full = e.hessian(u)
+        shard = e.hessian(u + 1e-3, zigzag_rows(Nt - 2, 1, 3))
+        fid = e.fidelities()
+        xih = e.state(2, 3)
+        out[mode] = (full, shard, fid, xih)
+        e.close()
+    for a, b in zip(out["0"][:2], out["1"][:2]):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    assert np.array_equal(out["0"][2], out["1"][2])
+    assert np.array_equal(out["0"][3].data, out["1"][3].data)
+    H = out["1"][0][0]
+    assert np.abs(H - c4["s32/H"]).max() <= 1e-6 * np.abs(c4["s32/H"]).max()
