@@ -65,7 +65,7 @@ def main():
     ap.add_argument("--group-m", type=int, default=40, help="GROUP basis size of the c4rows workload (0: GRAPE)")
     ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c4rows", "c5rows"], default="hessian")
     ap.add_argument("--c4-nt", type=int, default=33)
-    ap.add_argument("--c5-nt", type=int, default=5)
+    ap.add_argument("--c5-nt", type=int, default=17)
     ap.add_argument("--c5-warm", type=int, default=230)
     ap.add_argument("--controls", type=int, default=1,
                     help="K control vectors per GPU evaluated concurrently (K contexts, one host thread and "

@@ -2478,6 +2478,18 @@ hbm::Engine& pipe_worker(hbm_engine* h, int k) {
   W->gcst.imag = 0;
   return *W;
 }
+// OCG_PIPE_DEBUG=1: progress lines of the three stages on stderr (diagnostic)
+bool pipe_debug() {
+  static const bool d = std::getenv("OCG_PIPE_DEBUG") != nullptr;
+  return d;
+}
+#define PIPE_LOG(...)                          \
+  do {                                          \
+    if (pipe_debug()) {                         \
+      std::fprintf(stderr, __VA_ARGS__);        \
+      std::fflush(stderr);                      \
+    }                                           \
+  } while (0)
 // first slot of the row states and the slots the pipeline needs in total
 int pipe_psih_base(const hbm_engine* h, int N) { return 4 + 3 * N + 2; }
 }  // namespace
@@ -2529,10 +2541,12 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
           for (int s = 0; s + 1 < N && !abort_.load(); ++s) {
             W.step(c1, {u[N - 1 - s]}, {u[N - 2 - s]}, {0});
             W.store_many({&E.states[h->xi_base() + N - 2 - s]}, c1);
+            PIPE_LOG("[pipe X] xi step %d\n", s);
           }
           W.sync();
           W.release(c1[0]);
         }
+        PIPE_LOG("[pipe X] xi done, xiH in batches of %d\n", B);
         for (int t0 = 0; t0 < N && !abort_.load(); t0 += B) {
           const int nb = std::min(B, N - t0);
           std::vector<View> in;
@@ -2584,6 +2598,7 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
           W.sync();
           for (auto* c : out) W.release(c);
           psih_ready.store(end, std::memory_order_release);
+          PIPE_LOG("[pipe H] rows ready %d of %d\n", end, nrows);
           next = end;
         }
       } catch (...) {
@@ -2646,10 +2661,12 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
           fw.push_back(1);
           ss.push_back(&E.states[rsoff[r.k] + (r.t - rs[r.k])]);
         }
-        if (cs.empty()) {  // everything joined so far is done: wait for the next row
+        if (cs.empty()) {  // everything joined so far is done: wait for the next row, if any
+          if (joined >= nrows) break;
           wait_for(psih_ready, joined + 1);
           continue;
         }
+        PIPE_LOG("[pipe A] step batch %zu (psi t %d, rows %zu, joined %d)\n", cs.size(), tpsi, act.size(), joined);
         E.step(cs, uf, ut, fw);
         E.store_many(ss, cs);
         E.sync();
@@ -2667,8 +2684,10 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
       ex[0] = std::current_exception();
       abort_.store(1);
     }
+    PIPE_LOG("[pipe A] done, joining\n");
     tx.join();
     th.join();
+    PIPE_LOG("[pipe] joined\n");
     for (auto& e : ex)
       if (e) std::rethrow_exception(e);
     for (hbm::Engine* W : {&WH, &WX}) {  // the workers' GEMM statistics belong to this context

@@ -231,3 +231,26 @@ def test_c4_s32_pipelined_equals_stored(c4, monkeypatch):
     assert np.array_equal(out["0"][3].data, out["1"][3].data)
     H = out["1"][0][0]
     assert np.abs(H - c4["s32/H"]).max() <= 1e-6 * np.abs(c4["s32/H"]).max()
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_c4_w256_hessian_vs_oracle(c4, warm256, monkeypatch, pipe):
+    """config 4's real bond dimension (Maxm 256, the saturated warm state), N_t = 5:
+    divT, F, the GRAPE gradient and the full fidelity Hessian against the oracle
+    (tests/golden/make_c4_fixtures.py w256h: ~1 h on the CPU restatement) at the
+    north_star tolerances, through the pipelined and the stored getHessian"""
+    from optimalcontrolmps_amd.native import Engine
+    if "w256h/H" not in c4:
+        pytest.skip("w256h oracle fixture not generated")
+    monkeypatch.setenv("OCG_HBM_PIPE", pipe)
+    u = c4["w256h/u"]
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    eng.set_states(_mps(c4["w256h/tgt_dims"], c4["w256h/tgt_data"]), warm256)
+    H, divT, F = eng.hessian(u)
+    g = DT * (divT * F * 1j).real
+    Fo, go, Ho = complex(c4["w256h/F"][0]), c4["w256h/grad"], c4["w256h/H"]
+    assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12
+    assert np.abs(divT - c4["w256h/divT"]).max() <= 1e-8 * np.abs(c4["w256h/divT"]).max()
+    assert np.abs(g - go).max() <= 1e-6
+    assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+    eng.close()

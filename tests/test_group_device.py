@@ -83,13 +83,13 @@ def test_hessian_reuses_gradient_trajectories(states):
     u = np.random.default_rng(93).uniform(2, 10, 21)
     eng = Engine(L, p, N, J, 0.01, 1e-8, 80, engine="hbm")
     eng.set_states(st(50.0), st(2.5))
-    H0, d0, F0 = eng.hessian(u)                 # fresh
+    H0, d0, F0 = eng.hessian(u)                 # fresh (pipelined: hbm_hessian_pipe, stats kind 5)
     eng.propagate(u, 3)                          # the gradient's propagation
-    s0 = eng.stats(0)["launches"]
-    H1, d1, F1 = eng.hessian(u)                  # reuses psi_t / xi_t
-    assert eng.stats(0)["launches"] == s0
+    s0, p0 = eng.stats(0)["launches"], eng.stats(5)["launches"]
+    H1, d1, F1 = eng.hessian(u)                  # reuses psi_t / xi_t (no propagation, no pipeline)
+    assert eng.stats(0)["launches"] == s0 and eng.stats(5)["launches"] == p0
     assert np.array_equal(H0, H1) and np.array_equal(d0, d1) and F0 == F1
     u2 = u.copy()
     u2[5] += 1e-3
     eng.hessian(u2)                              # a new control propagates again
-    assert eng.stats(0)["launches"] > s0
+    assert eng.stats(0)["launches"] + eng.stats(5)["launches"] > s0 + p0
