@@ -463,7 +463,10 @@ def bench_c4(args):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     gm = eng.stats(7)   # k_gemm: the MFMA-FP64 contraction kernel
-    st_traj = eng.stats(0)
+    # one bare psi chain (ocg_propagate(u, 1)) outside the timed region: the single-chain step rate
+    t_sc = time.perf_counter()
+    eng.propagate(control(nsteps_all), 1)
+    t_sc = time.perf_counter() - t_sc
     steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
     row_steps = (Nt - 2) * (Nt - 3) // 2
     reps = 1 if strong else world   # independent Hessians / gradients per step
@@ -494,7 +497,7 @@ def bench_c4(args):
                                     + f" over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)"),
                        "engine": "HBM-resident (hbm.hip)", "parallelism": par},
             "sweep_steps_per_sec": sweep / elapsed,
-            "single_chain_steps_per_sec": 1e3 * (Nt - 1) / max(st_traj["ms"] / max(1, st_traj["launches"]), 1e-9),
+            "single_chain_steps_per_sec": (Nt - 1) / t_sc,
             "mfma_gemm": {"kernel": "k_gemm (v_mfma_f64_16x16x4f64)", "launches_per_step": gm["launches"] / args.steps,
                           "avg_launch_ms": gemm_ms, "share_of_time": gm["ms"] / (1e3 * elapsed),
                           "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,

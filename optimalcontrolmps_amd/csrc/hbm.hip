@@ -208,6 +208,13 @@ struct Engine {
   // smallest Gram order on the blocked kernel k_heev_vals_big (default: the orders the register
   // kernels cannot hold); OCG_HBM_BIGMIN overrides (tests; > kBigMax: the eager L2 kernel, A/B)
   int big_min = std::getenv("OCG_HBM_BIGMIN") ? std::atoi(std::getenv("OCG_HBM_BIGMIN")) : RNMAX + 1;
+  // Maxm-boundary eigenvalue resolution (k_heev_thresh + k_heev_bisect) for
+  // register-path Gram blocks of order >= thresh_min; OCG_HBM_THRESH=0: off,
+  // OCG_HBM_THRESH=n > 1: the smallest order
+  bool thresh_on = !std::getenv("OCG_HBM_THRESH") || std::atoi(std::getenv("OCG_HBM_THRESH")) != 0;
+  int thresh_min = (std::getenv("OCG_HBM_THRESH") && std::atoi(std::getenv("OCG_HBM_THRESH")) > 1)
+                       ? std::atoi(std::getenv("OCG_HBM_THRESH"))
+                       : 48;
   double phase_ms[8] = {0};
   long phase_n[8] = {0};
   double steps_done[8] = {0};
@@ -753,6 +760,29 @@ struct Engine {
       return;
     }
     gemm(gt, gs);
+    // Maxm boundary first (k_heev_thresh), then only the eigenvalues above it
+    // (k_heev_bisect) for the register-path sectors of decompositions in which
+    // Maxm can bind; OCG_HBM_THRESH=0 turns it off (A/B)
+    std::vector<int> thr_items, deferred;
+    int max_def = 0;
+    if (thresh_on) {
+      for (size_t j = 0; j < jobs.size(); ++j) {
+        int T = 0;
+        for (int i = R.job_p0[j]; i < R.job_p0[j + 1]; ++i) T += R.probs[i].n;
+        if (T <= jobs[j].maxm + 1) continue;
+        bool any = false;
+        for (int i = R.job_p0[j]; i < R.job_p0[j + 1]; ++i) {
+          const int n = R.probs[i].n;
+          if (n >= std::max(reg_min, thresh_min) && n <= RNMAX && n < big_min) {
+            R.probs[i].defer = 1;
+            deferred.push_back(i);
+            max_def = std::max(max_def, n);
+            any = true;
+          }
+        }
+        if (any) thr_items.push_back(int(j));
+      }
+    }
     R.d_probs = upload(R.probs);
     // bounds: device copy, then point the items at it
     const int* d_bounds = upload(bounds);
@@ -793,6 +823,13 @@ struct Engine {
       if (!order.empty()) {
         hipLaunchKernelGGL(k_heev_vals_any, dim3(int(order.size())), dim3(RNT), lds_v, st, R.d_probs, upload(order),
                            reg_min);
+        HCK(hipGetLastError());
+      }
+      if (!thr_items.empty()) {
+        hipLaunchKernelGGL(k_heev_thresh, dim3(int(thr_items.size())), dim3(THN), thresh_lds_bytes(), st, d_items,
+                           upload(thr_items), const_cast<EProb*>(R.d_probs));
+        hipLaunchKernelGGL(k_heev_bisect, dim3(int(deferred.size())), dim3(BSN), bisect_lds_bytes(max_def), st,
+                           R.d_probs, upload(deferred));
         HCK(hipGetLastError());
       }
       if (!big.empty()) HCK(hipStreamWaitEvent(st, ev_join, 0));  // join before the truncation

@@ -308,6 +308,9 @@ struct EProb {
   // eigenvalues below thr_rel * trace may be left unresolved (k_heev_vals_reg):
   // they are provably inside the discarded tail of the truncation (hbm_eig.hpp)
   double thr_rel;
+  // 1: the register kernel leaves the eigenvalues to k_heev_bisect, after
+  // k_heev_thresh has raised thr_rel to the decomposition's Maxm boundary
+  int defer;
 };
 
 template <class T>

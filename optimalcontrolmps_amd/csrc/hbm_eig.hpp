@@ -438,9 +438,132 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
   double* hi = lo + NM;
   int* cnt = (int*)(hi + NM);
 #ifndef HBM_NO_BISECT  // timing builds of tools/eig_bench only
-  bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt);
+  if (!P.defer) bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt);
 #endif
 }
+
+// ------------------------------------------------- Maxm boundary, then bisection
+// When Maxm can bind (a decomposition with more than Maxm + 1 eigenvalues),
+// the truncation keeps at most the Maxm largest of all its sectors' eigenvalues
+// and needs the others only through their sum (trace - resolved: exact), so the
+// sectors' eigenvalues below the (Maxm + 1)-th largest never have to be
+// resolved.  k_heev_thresh brackets that eigenvalue for one decomposition by
+// multisection over the union of its sectors' tridiagonals (Sturm counts
+// summed over sectors), and raises each deferred sector's thr_rel to 0.999 x
+// the bracket's lower end; k_heev_bisect then resolves only the eigenvalues
+// above it (bisect_all: the others are set to their mean, below the
+// threshold, so they rank behind every kept one and the suffix sums of the
+// truncation rule stay exact).
+constexpr int THN = 1024;          // threads of k_heev_thresh
+constexpr int THC = 32;            // candidate shifts per multisection round
+constexpr int kThrMaxT = 5120;     // eigenvalues of one decomposition (= kMaxEig)
+__global__ __launch_bounds__(THN) void k_heev_thresh(const TItem* __restrict__ items, const int* __restrict__ which,
+                                                    EProb* __restrict__ probs) {
+  extern __shared__ __align__(16) char smem_th[];
+  const TItem I = items[which[blockIdx.x]];
+  const int tid = threadIdx.x, np = I.np;
+  double* Ld = reinterpret_cast<double*>(smem_th);  // every sector's d, then e^2
+  double* Le2 = Ld + kThrMaxT;
+  __shared__ int off[65], cnt[THC];
+  __shared__ double tr[64], piv[64], gub[64], sx[2];
+  if (tid == 0) {
+    int o = 0;
+    for (int q = 0; q < np; ++q) { off[q] = o; o += probs[I.p0 + q].n; }
+    off[np] = o;
+  }
+  __syncthreads();
+  const int T = off[np];
+  for (int q = 0; q < np; ++q) {
+    const EProb& P = probs[I.p0 + q];
+    for (int i = tid; i < P.n; i += THN) {
+      Ld[off[q] + i] = P.d[i];
+      Le2[off[q] + i] = P.e[i] * P.e[i];
+    }
+  }
+  __syncthreads();
+  // per sector: trace, Gershgorin upper bound, pivmin (one wave per sector)
+  const int wv = tid >> 6, lane = tid & 63;
+  for (int q = wv; q < np; q += THN / 64) {
+    const int n = off[q + 1] - off[q];
+    const double* d = Ld + off[q];
+    const double* e2 = Le2 + off[q];
+    double t = 0, g = -1e300, em = 0;
+    for (int i = lane; i < n; i += 64) {
+      const double el = i > 0 ? sqrt(e2[i - 1]) : 0.0, er = i + 1 < n ? sqrt(e2[i]) : 0.0;
+      t += d[i];
+      g = fmax(g, d[i] + el + er);
+      em = fmax(em, e2[i]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      t += __shfl_xor(t, o, 64);
+      g = fmax(g, __shfl_xor(g, o, 64));
+      em = fmax(em, __shfl_xor(em, o, 64));
+    }
+    if (lane == 0) { tr[q] = t; gub[q] = g; piv[q] = 2.2250738585072014e-308 * fmax(1.0, em); }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double g = 0;
+    for (int q = 0; q < np; ++q) g = fmax(g, gub[q]);
+    sx[0] = 0.0;              // lo: count(lambda > lo) >= target
+    sx[1] = g * (1.0 + 1e-12) + 1e-300;  // hi: count(lambda > hi) < target
+  }
+  __syncthreads();
+  const int target = I.maxm + 1;
+  for (int round = 0; round < 12; ++round) {
+    const double lo = sx[0], hi = sx[1];
+    if (!(hi - lo > 1e-3 * hi)) break;  // uniform
+    if (tid < THC) cnt[tid] = 0;
+    __syncthreads();
+    // (sector, candidate) pairs: count of eigenvalues above x_c = n - #below
+    for (int pr = tid; pr < np * THC; pr += THN) {
+      const int q = pr / THC, c = pr - q * THC;
+      const int n = off[q + 1] - off[q];
+      if (n <= 0) continue;
+      const double x = lo + (hi - lo) * double(c + 1) / double(THC + 1);
+      const int below = sturm(Ld + off[q], Le2 + off[q], n, x, piv[q]);
+      atomicAdd(&cnt[c], n - below);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double nlo = lo, nhi = hi;
+      for (int c = 0; c < THC; ++c) {
+        const double x = lo + (hi - lo) * double(c + 1) / double(THC + 1);
+        if (cnt[c] >= target) nlo = x;
+        else { nhi = x; break; }
+      }
+      sx[0] = nlo;
+      sx[1] = nhi;
+    }
+    __syncthreads();
+  }
+  const double thr = 0.999 * sx[0];
+  if (T > target && thr > 0)
+    for (int q = tid; q < np; q += THN) {
+      EProb& P = probs[I.p0 + q];
+      if (P.defer && tr[q] > 0) P.thr_rel = fmax(P.thr_rel, thr / tr[q]);
+    }
+}
+__host__ __device__ constexpr int thresh_lds_bytes() { return 2 * kThrMaxT * 8; }
+
+constexpr int BSN = 512;  // threads of k_heev_bisect
+__global__ __launch_bounds__(BSN) void k_heev_bisect(const EProb* __restrict__ probs, const int* __restrict__ idx) {
+  extern __shared__ __align__(16) char smem_bs[];
+  const EProb P = probs[idx[blockIdx.x]];
+  const int n = P.n, tid = threadIdx.x;
+  double* Ld = reinterpret_cast<double*>(smem_bs);
+  double* Le2 = Ld + n;
+  double* lo = Le2 + n;
+  double* hi = lo + n;
+  int* cnt = reinterpret_cast<int*>(hi + n);
+  for (int i = tid; i < n; i += BSN) {
+    Ld[i] = P.d[i];
+    Le2[i] = P.e[i] * P.e[i];
+  }
+  __syncthreads();
+  bisect_all<BSN>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt);
+}
+__host__ __device__ constexpr int bisect_lds_bytes(int n) { return 4 * n * 8 + 4 * BSN * 4 + 64; }
 
 // One launch per decomposition: each workgroup picks the variant for its
 // block's order (register slot grid 2 / 4 / 8 / 12 / 13, or the LDS / L2
