@@ -209,9 +209,11 @@ struct Engine {
   // kernels cannot hold); OCG_HBM_BIGMIN overrides (tests; > kBigMax: the eager L2 kernel, A/B)
   int big_min = std::getenv("OCG_HBM_BIGMIN") ? std::atoi(std::getenv("OCG_HBM_BIGMIN")) : RNMAX + 1;
   // Maxm-boundary eigenvalue resolution (k_heev_thresh + k_heev_bisect) for
-  // register-path Gram blocks of order >= thresh_min; OCG_HBM_THRESH=0: off,
-  // OCG_HBM_THRESH=n > 1: the smallest order
-  bool thresh_on = !std::getenv("OCG_HBM_THRESH") || std::atoi(std::getenv("OCG_HBM_THRESH")) != 0;
+  // register-path Gram blocks of order >= thresh_min; OCG_HBM_THRESH=1: on,
+  // OCG_HBM_THRESH=n > 1: on from order n.  Off by default: at config 4 the two
+  // extra launches per decomposition cost more than the shorter multisection
+  // saves (c4rows N_t = 33: 2138 vs 2055 ms per getHessian)
+  bool thresh_on = std::getenv("OCG_HBM_THRESH") && std::atoi(std::getenv("OCG_HBM_THRESH")) != 0;
   int thresh_min = (std::getenv("OCG_HBM_THRESH") && std::atoi(std::getenv("OCG_HBM_THRESH")) > 1)
                        ? std::atoi(std::getenv("OCG_HBM_THRESH"))
                        : 48;
@@ -760,9 +762,9 @@ struct Engine {
       return;
     }
     gemm(gt, gs);
-    // Maxm boundary first (k_heev_thresh), then only the eigenvalues above it
-    // (k_heev_bisect) for the register-path sectors of decompositions in which
-    // Maxm can bind; OCG_HBM_THRESH=0 turns it off (A/B)
+    // OCG_HBM_THRESH: Maxm boundary first (k_heev_thresh), then only the
+    // eigenvalues above it (k_heev_bisect) for the register-path sectors of
+    // decompositions in which Maxm can bind
     std::vector<int> thr_items, deferred;
     int max_def = 0;
     if (thresh_on) {
@@ -826,6 +828,8 @@ struct Engine {
         HCK(hipGetLastError());
       }
       if (!thr_items.empty()) {
+        // the boundary counts read every sector's tridiagonal, the blocked kernel's too
+        if (!big.empty()) HCK(hipStreamWaitEvent(st, ev_join, 0));
         hipLaunchKernelGGL(k_heev_thresh, dim3(int(thr_items.size())), dim3(THN), thresh_lds_bytes(), st, d_items,
                            upload(thr_items), const_cast<EProb*>(R.d_probs));
         hipLaunchKernelGGL(k_heev_bisect, dim3(int(deferred.size())), dim3(BSN), bisect_lds_bytes(max_def), st,

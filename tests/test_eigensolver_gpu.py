@@ -98,25 +98,25 @@ def test_lds_engine_refuses(states):
 
 
 def test_maxm_boundary_threshold(eng, monkeypatch):
-    """decompositions with more than Maxm + 1 eigenvalues resolve only those above
-    the (Maxm + 1)-th largest (k_heev_thresh + k_heev_bisect): Maxm binding
-    (slow spectrum) and the cutoff binding first (fast spectrum, the rule's
-    suffix sums from the exact trace), against numpy, and against the path that
-    resolves every eigenvalue (OCG_HBM_THRESH=0): same kept counts, same factors
-    to rounding"""
+    """OCG_HBM_THRESH=1: decompositions with more than Maxm + 1 eigenvalues
+    resolve only those above the (Maxm + 1)-th largest (k_heev_thresh +
+    k_heev_bisect): Maxm binding (slow spectrum) and the cutoff binding first
+    (fast spectrum, the rule's suffix sums from the exact trace), against numpy,
+    and against the default path that resolves every eigenvalue: same kept
+    counts, same factors to rounding"""
     from optimalcontrolmps_amd.native import Engine
     rng = np.random.default_rng(2024)
     Ms = [block(rng, 200, 260, np.exp(-np.arange(200) / 15.0)),
           block(rng, 200, 200, np.exp(-np.arange(200) / 3.0)),
           block(rng, 150, 180, np.exp(-np.arange(150) / 8.0))]
-    res = eng.denmat_decomp(Ms, 1e-8, 60)
+    monkeypatch.setenv("OCG_HBM_THRESH", "1")
+    e1 = Engine(L, p, NPART, 1.0, 0.005, 1e-8, 512, engine="hbm")
+    res = e1.denmat_decomp(Ms, 1e-8, 60)
+    e1.close()
     for M, r in zip(Ms, res):
         check(M, r, 1e-8, 60)
     assert res[0][0] == 60 and res[1][0] < 60
-    monkeypatch.setenv("OCG_HBM_THRESH", "0")
-    e0 = Engine(L, p, NPART, 1.0, 0.005, 1e-8, 512, engine="hbm")
-    ref = e0.denmat_decomp(Ms, 1e-8, 60)
-    e0.close()
+    ref = eng.denmat_decomp(Ms, 1e-8, 60)
     for r, r0 in zip(res, ref):
         assert r[0] == r0[0]
         assert np.abs(r[2] @ r[3] - r0[2] @ r0[3]).max() <= 1e-12 * np.abs(r0[2] @ r0[3]).max()
