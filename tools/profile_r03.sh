@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-3 rocprofv3 evidence (kernel trace + FETCH / WRITE / MFMA-issue PMC passes,
+# tools/profile_r02.sh) of the bench commands whose lines carry a roofline:
+#   r03       python bench.py (config 1, the driver's default line)
+#   r03c4n33  python bench.py --workload c4rows (pipelined HBM getHessian, GROUP M=40)
+#   r03c5n17  python bench.py --workload c5rows
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+for w in ${@:-c1 c4 c5}; do
+  case $w in
+    c1) bash $R/tools/profile_r02.sh r03 --no-cpu-baseline --steps 5 --warmup 1 || exit $? ;;
+    c4) bash $R/tools/profile_r02.sh r03c4n33 --workload c4rows --steps 1 --warmup 1 || exit $? ;;
+    c5) bash $R/tools/profile_r02.sh r03c5n17 --workload c5rows --steps 1 --warmup 0 || exit $? ;;
+  esac
+  echo "profiled $w"
+done
