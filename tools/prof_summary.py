@@ -40,9 +40,17 @@ def pmc(db, counter):
     return out
 
 
+def db(kind, tag):
+    """rocpd database of one pass: $PROF_DB_ROOT/<kind>/ (tools/profile_r02.sh) or
+    gpurun_out/<kind>_<tag>/ (older layout)"""
+    root = os.environ.get("PROF_DB_ROOT")
+    if root:
+        return os.path.join(root, kind, "run_results.db")
+    return os.path.join(ROOT, "gpurun_out", f"{kind}_{tag}", "run_results.db")
+
+
 def main(tag, outdir=None):
-    g = os.path.join(ROOT, "gpurun_out")
-    ks = kernel_stats(os.path.join(g, f"prof_{tag}", "run_results.db"))
+    ks = kernel_stats(db("prof", tag))
     prof = outdir or os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
@@ -50,8 +58,8 @@ def main(tag, outdir=None):
         w.writeheader()
         for r in ks:
             w.writerow(r)
-    fetch = pmc(os.path.join(g, f"pmc_fetch_{tag}", "run_results.db"), "FETCH_SIZE")
-    write = pmc(os.path.join(g, f"pmc_write_{tag}", "run_results.db"), "WRITE_SIZE")
+    fetch = pmc(db("pmc_fetch", tag), "FETCH_SIZE")
+    write = pmc(db("pmc_write", tag), "WRITE_SIZE")
     per = {}
     with open(os.path.join(prof, f"{tag}_pmc.csv"), "w", newline="") as f:
         w = csv.writer(f)
@@ -65,7 +73,7 @@ def main(tag, outdir=None):
             per[k] = dict(dispatches=fk[1], fetch_kb=f_kb, write_kb=w_kb, hbm_bytes=corrected)
             w.writerow([k, fk[1], f"{f_kb:.3f}", f"{w_kb:.3f}", f"{corrected:.0f}"])
     extra = {}
-    mdb = os.path.join(g, f"pmc_mfma_{tag}", "run_results.db")
+    mdb = db("pmc_mfma", tag)
     if os.path.exists(mdb):
         for cn in ("SQ_INSTS_VALU_MFMA_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
                    "SQ_INSTS_VALU_FMA_F64", "GRBM_GUI_ACTIVE"):
