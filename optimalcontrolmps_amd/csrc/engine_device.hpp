@@ -361,6 +361,7 @@ struct Chain {
   int ph_dir = -1;
   unsigned long long pf_last = 0;
   int pf_cur = 0;
+  int pf_gauge = 0;  // profile build: cycles inside gauge moves also go to PROF[31]
   // algorithmic-traffic model accumulators (per lane, summed at the end)
   double m_bytes = 0, m_flops = 0;
 
@@ -430,7 +431,10 @@ struct Chain {
 #ifdef OCG_PROFILE
     if (tid == 0) {
       unsigned long long t = __builtin_amdgcn_s_memtime();
-      if (pf_last) PROF[pf_cur] += double(t - pf_last);
+      if (pf_last) {
+        PROF[pf_cur] += double(t - pf_last);
+        if (pf_gauge) PROF[31] += double(t - pf_last);
+      }
       pf_last = t;
       pf_cur = cat;
     }
@@ -2136,8 +2140,12 @@ struct Chain {
   __device__ OCG_INLINE void position(int& centre, int target, int* gslot = nullptr) {
     while (centre != target) {
       const int slot = gslot ? P.ngates + (*gslot)++ : -1;
+      pf(pf_cur);
+      pf_gauge = 1;
       if (centre < target) { gauge_right(centre, OCG_GAUGE_CUTOFF, 1 << 30, slot); ++centre; }
       else { gauge_left(centre, OCG_GAUGE_CUTOFF, 1 << 30, slot); --centre; }
+      pf(pf_cur);
+      pf_gauge = 0;
     }
   }
 

@@ -43,6 +43,7 @@ for what in ["trajectory(2 chains x 200 steps)", "div_t+xi_dH", "hessian_rows(19
     for i, n in sorted(NAMES.items()):
         if pr[i] > 0:
             print(f"   {n:12s} {pr[i]:.3e} ({100*pr[i]/tot:5.1f}%)")
+    print(f"   (inside gauge moves: {pr[31]:.3e} = {100*pr[31]/max(tot,1):.1f}% of the cycles)")
     if pr[21] > 0:
         print(f"   jacobi calls {pr[21]:.0f}, sweeps/call {pr[20]/pr[21]:.2f}, rounds/sweep {pr[22]/pr[21]:.2f}, "
               f"rounds executed/call (wave 0 of the first block group) {pr[30]/pr[21]:.2f}")
