@@ -589,17 +589,17 @@ __global__ __launch_bounds__(RNT, 1) void k_heev_vals_any(const EProb* __restric
 // ------------------------------------------------------------------ vectors
 // Kept eigenvectors U = Q D Z (n x k, ld k) of one problem per workgroup.
 // Fast path (n <= RNMAX, k <= 64, Z fits LDS): inverse iteration on the real
-// tridiagonal (one lane per eigenvalue; LDL^T pivots in P.Dv), classical
-// Gram-Schmidt twice in descending order with Z in LDS, then U = D Z in
-// registers (lane = column, rows i = 8a + wave) and the reflectors applied
-// j = n-2 .. 0 from LDS blocks.  Other sizes: the same algorithm with Z and
-// U in global memory.
+// tridiagonal (one lane per eigenvalue), CholeskyQR2 of the k vectors with Z
+// in LDS (classical Gram-Schmidt twice if a Cholesky pivot collapses), then
+// U = D Z in registers (lane = column, rows i = 8a + wave) and the reflectors
+// applied j = n-2 .. 0 from LDS blocks.  Other sizes: the same algorithm with
+// Z in global memory (pivots in P.Dv) and U by k_heev_bt.
 constexpr int kVecLds = 143360;  // bytes of the Z + pivot / Gram / reflector-block region
-// Inverse iteration for lane-parallel eigenvectors with the pivots in LDS
-// (column jd of Dv, ld ldd): pivots by a refined reciprocal, the forward and
-// backward sweeps unrolled by 4 with their loads issued ahead of the
-// dependent FMA chain (one wave carries the whole batch: no other wave hides
-// LDS latency).
+// Inverse iteration for eigenvalue lam into column jz of Z (ld ldz), one
+// thread per eigenvalue, LDL^T pivots in column jd of Dv (ld ldd), LDS or
+// global: pivots by a refined reciprocal, the forward and backward sweeps
+// unrolled by 4 with their loads issued ahead of the dependent FMA chain (few
+// threads carry the whole batch: nothing else hides the memory latency).
 __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const double* __restrict__ Le, int n,
                                            double lam, double tiny, double* __restrict__ Z, int ldz, int jz,
                                            double* __restrict__ Dv, int ldd, int jd, int jj) {
@@ -689,45 +689,35 @@ __device__ __forceinline__ T block_sum_r(T v, T* red) {
   return s;
 }
 
-// inverse iteration for eigenvalue lam into column jz of Z (ld ldz), LDL^T
-// pivots in column jd of Dv (ld ldd), starting vector hashed from (i, jj)
-__device__ __forceinline__ void invit(const double* Ld, const double* Le, int n, double lam, double tiny, double* Z,
-                                      int ldz, int jz, double* Dv, int ldd, int jd, int jj) {
-  double q = Ld[0] - lam;
-  if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
-  Dv[jd] = q;
-  for (int i = 1; i < n; ++i) {
-    q = Ld[i] - lam - Le[i - 1] * Le[i - 1] / q;
-    if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
-    Dv[(size_t)i * ldd + jd] = q;
-  }
-  for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] = hrand(i, jj);
-  for (int it = 0; it < 3; ++it) {
-    double y = Z[jz], qp = Dv[jd];
-    for (int i = 1; i < n; ++i) {
-      const size_t o = (size_t)i * ldz + jz;
-      y = Z[o] - Le[i - 1] / qp * y;
-      Z[o] = y;
-      qp = Dv[(size_t)i * ldd + jd];
+// Right-looking Cholesky G = L L^T of the lower triangle of G (order k, ld
+// ldg, LDS) by the whole workgroup: per column, every thread reads the pivot,
+// threads over rows scale the column, a barrier, then waves over rows and
+// lanes over columns apply the rank-1 update (and one thread stores the
+// diagonal, which nothing reads until the next column), a barrier.  The same
+// operations in the same order per element as a one-wave Cholesky, with two
+// barriers per column instead of k dependent LDS round trips.  false
+// (uniform): a pivot <= 1e-10 (the columns are unit vectors: a near
+// dependency).  Caller: barrier before (G written), none needed after.
+__device__ __forceinline__ bool chol_wg(double* G, int ldg, int k) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  for (int cc = 0; cc < k; ++cc) {
+    const double dgg = G[cc * ldg + cc];
+    if (!(dgg > 1e-10)) return false;
+    const double dd = sqrt(dgg);
+    for (int i = cc + 1 + tid; i < k; i += VNT) G[i * ldg + cc] = G[i * ldg + cc] / dd;
+    __syncthreads();
+    if (tid == 0) G[cc * ldg + cc] = dd;
+    for (int i = cc + 1 + wv; i < k; i += VNT / 64) {
+      const double li = G[i * ldg + cc];
+      for (int jj = cc + 1 + lane; jj <= i; jj += 64) G[i * ldg + jj] = fma(-li, G[jj * ldg + cc], G[i * ldg + jj]);
     }
-    double xn = Z[(size_t)(n - 1) * ldz + jz] / Dv[(size_t)(n - 1) * ldd + jd];
-    Z[(size_t)(n - 1) * ldz + jz] = xn;
-    double ss = xn * xn;
-    for (int i = n - 2; i >= 0; --i) {
-      const size_t o = (size_t)i * ldz + jz;
-      xn = (Z[o] - Le[i] * xn) / Dv[(size_t)i * ldd + jd];
-      Z[o] = xn;
-      ss += xn * xn;
-    }
-    const double inv = ss > 0 ? 1.0 / sqrt(ss) : 0.0;
-    for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] *= inv;
+    __syncthreads();
   }
+  return true;
 }
-
 
 __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__ probs, int nprob) {
   __shared__ __align__(16) char un[kVecLds];
-  __shared__ int chol_fail;
   __shared__ double Ld[RNMAX], Le[RNMAX], Lc[64];
   __shared__ z part[VNT / 64][64];
   __shared__ double red[VNT / 64];
@@ -778,7 +768,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
       if (tid < batch && jj < k) invit_fast(Ld, Le, n, P.w[jj], tiny, Zl, ldz, jj, piv, batch, tid, jj);
     }
   } else {
-    for (int jj = tid; jj < k; jj += VNT) invit(Gd, Ge, n, P.w[jj], tiny, Z, lz, jj, P.Dv, n, jj, jj);
+    for (int jj = tid; jj < k; jj += VNT) invit_fast(Gd, Ge, n, P.w[jj], tiny, Z, lz, jj, P.Dv, n, jj, jj);
   }
   __syncthreads();
   STAMP(0);
@@ -806,32 +796,8 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
         for (int t = 0; t < 8; ++t)
           if (8 * jb + t <= i) G[i * 65 + 8 * jb + t] = acc[t];
       }
-      if (tid == 0) chol_fail = 0;
       __syncthreads();
-      if (wv == 0) {
-        // right-looking Cholesky, lane i owns row i
-        for (int cc = 0; cc < k; ++cc) {
-          const double dgg = G[cc * 65 + cc];
-          if (!(dgg > 1e-10)) {  // columns are unit vectors: a pivot this small means a near dependency
-            if (lane == 0) chol_fail = 1;
-            break;
-          }
-          const double dd = sqrt(dgg);
-          if (lane == cc) G[cc * 65 + cc] = dd;
-          const double lic = (lane > cc && lane < k) ? G[lane * 65 + cc] / dd : 0.0;
-          if (lane > cc && lane < k) G[lane * 65 + cc] = lic;
-          __builtin_amdgcn_wave_barrier();
-          // trailing update, uniform trip count so the independent LDS loads pipeline
-#pragma unroll 8
-          for (int jj = cc + 1; jj < k; ++jj) {
-            const double ljc = G[jj * 65 + cc];
-            if (jj <= lane && lane < k) G[lane * 65 + jj] = fma(-lic, ljc, G[lane * 65 + jj]);
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-      __syncthreads();
-      if (chol_fail) { need_gs = true; break; }
+      if (!chol_wg(G, 65, k)) { need_gs = true; break; }
       // Z[r][:] <- Z[r][:] L^-T: forward substitution along the row
       for (int rr = tid; rr < n; rr += VNT) {
         double* zr = Zl + (size_t)rr * ldz;
@@ -893,45 +859,11 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
         for (int t = 0; t < 8; ++t)
           if (8 * jb + t <= i) G[i * ldg + 8 * jb + t] = acc[q][t];
       }
-      if (tid == 0) chol_fail = 0;
       __syncthreads();
-      if (wv == 0) {
-        // right-looking Cholesky, lane owns rows lane and lane + 64
-        for (int cc = 0; cc < k; ++cc) {
-          const double dgg = G[cc * ldg + cc];
-          if (!(dgg > 1e-10)) {
-            if (lane == 0) chol_fail = 1;
-            break;
-          }
-          const double dd = sqrt(dgg);
-          double lic[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int row = lane + 64 * h;
-            lic[h] = (row > cc && row < k) ? G[row * ldg + cc] / dd : 0.0;
-          }
-          __builtin_amdgcn_wave_barrier();
-          if (lane == cc % 64 && cc / 64 == 0) G[cc * ldg + cc] = dd;
-          if (lane == cc % 64 && cc / 64 == 1) G[cc * ldg + cc] = dd;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int row = lane + 64 * h;
-            if (row > cc && row < k) G[row * ldg + cc] = lic[h];
-          }
-          __builtin_amdgcn_wave_barrier();
-          for (int jj = cc + 1; jj < k; ++jj) {
-            const double ljc = G[jj * ldg + cc];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int row = lane + 64 * h;
-              if (jj <= row && row < k) G[row * ldg + jj] = fma(-lic[h], ljc, G[row * ldg + jj]);
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-      __syncthreads();
-      if (chol_fail) { need_gs = true; break; }
+      STAMP(5);
+      const bool ok = chol_wg(G, ldg, k);
+      STAMP(6);
+      if (!ok) { need_gs = true; break; }
       // Z[r][:] <- Z[r][:] L^-T, one row per thread, 16 columns at a time in registers
       for (int rr = tid; rr < n; rr += VNT) {
         double* zr = Z + (size_t)rr * n;
@@ -939,11 +871,16 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
           double x[16];
 #pragma unroll
           for (int t = 0; t < 16; ++t) x[t] = b0 + t < k ? zr[b0 + t] : 0.0;
-          for (int i = 0; i < b0; ++i) {
-            const double zi = zr[i];
+          // the solved part of the row, 8 loads in flight per group (b0 is a multiple of 16)
+          for (int i = 0; i < b0; i += 8) {
+            double zv[8];
 #pragma unroll
-            for (int t = 0; t < 16; ++t)
-              if (b0 + t < k) x[t] = fma(-zi, G[(b0 + t) * ldg + i], x[t]);
+            for (int u = 0; u < 8; ++u) zv[u] = zr[i + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+              for (int t = 0; t < 16; ++t)
+                if (b0 + t < k) x[t] = fma(-zv[u], G[(b0 + t) * ldg + i + u], x[t]);
           }
 #pragma unroll
           for (int t = 0; t < 16; ++t) {
@@ -959,6 +896,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
         }
       }
       __syncthreads();
+      STAMP(7);
     }
   }
   if (need_gs) {
@@ -1001,7 +939,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
   STAMP(1);
   if (!fast && n <= kBtRows) {  // U = Q D Z by k_heev_bt
 #ifdef HBM_STAMP
-    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu\n", n, k, stamp_acc[0], stamp_acc[1]);
+    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu (gram %llu chol %llu solve %llu) gs %d\n", n, k, stamp_acc[0], stamp_acc[1], stamp_acc[5], stamp_acc[6], stamp_acc[7], int(need_gs));
 #endif
     return;
   }
