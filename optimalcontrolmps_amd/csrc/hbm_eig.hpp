@@ -716,6 +716,99 @@ __device__ __forceinline__ bool chol_wg(double* G, int ldg, int k) {
   return true;
 }
 
+// One CholeskyQR pass over the k columns of Z (n x k, ld ldz; LDS or global):
+// G = Z^T Z (lower triangle, ld ldg, LDS), G = L L^T (chol_wg), Z <- Z L^-T.
+// The Gram matrix and the solve's block updates run on the matrix cores
+// (v_mfma_f64_16x16x4f64: lane l holds A[l & 15][kk] and B[kk][l & 15],
+// kk = k-step + (l >> 4); the result C[(l >> 4) + 4 r][l & 15]), four
+// k-steps' loads in flight per wave; the solve goes by 16-column blocks b0:
+// Z_B -= Z_{<B} L_{B,<B}^T (waves over 16-row tiles), then every row's
+// 16 x 16 forward substitution against L_BB by one thread.  false (uniform):
+// a collapsed pivot (Z untouched by this pass).  Caller: barrier before.
+__device__ __forceinline__ bool cholqr_pass(double* Z, int ldz, int n, int k, double* G, int ldg) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int a16 = lane & 15, kq = lane >> 4;
+  {
+    const int T = (k + 15) >> 4, ntile = T * (T + 1) / 2;
+    for (int t = wv; t < ntile; t += VNT / 64) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      const int J = t - I * (I + 1) / 2;
+      const int ca = 16 * I + a16, cb = 16 * J + a16;
+      d4 acc = {0, 0, 0, 0};
+      for (int k0 = 0; k0 < n; k0 += 16) {
+        double va[4], vb[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int rr = k0 + 4 * s + kq;
+          va[s] = (rr < n && ca < k) ? Z[(size_t)rr * ldz + ca] : 0.0;
+          vb[s] = (rr < n && cb < k) ? Z[(size_t)rr * ldz + cb] : 0.0;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[s], vb[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I + kq + 4 * r;
+        if (row < k && cb < k && cb <= row) G[row * ldg + cb] = acc[r];
+      }
+    }
+  }
+  __syncthreads();
+  const bool ok = chol_wg(G, ldg, k);
+  if (!ok) return false;
+  for (int b0 = 0; b0 < k; b0 += 16) {
+    const int nb = k - b0 < 16 ? k - b0 : 16;
+    if (b0 > 0) {
+      for (int R = wv; 16 * R < n; R += VNT / 64) {
+        const int ra = 16 * R + a16, cb = b0 + a16;
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * R + kq + 4 * r;
+          acc[r] = (row < n && cb < k) ? Z[(size_t)row * ldz + cb] : 0.0;
+        }
+        for (int k0 = 0; k0 < b0; k0 += 16) {
+          double va[4], vb[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int kk = k0 + 4 * s + kq;
+            va[s] = ra < n ? -Z[(size_t)ra * ldz + kk] : 0.0;
+            vb[s] = cb < k ? G[cb * ldg + kk] : 0.0;
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[s], vb[s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * R + kq + 4 * r;
+          if (row < n && cb < k) Z[(size_t)row * ldz + cb] = acc[r];
+        }
+      }
+      __syncthreads();
+    }
+    for (int rr = tid; rr < n; rr += VNT) {
+      double* zr = Z + (size_t)rr * ldz + b0;
+      double x[16];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) x[t] = t < nb ? zr[t] : 0.0;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        if (t < nb) {
+#pragma unroll
+          for (int s2 = 0; s2 < t; ++s2) x[t] = fma(-x[s2], G[(b0 + t) * ldg + b0 + s2], x[t]);
+          x[t] = x[t] / G[(b0 + t) * ldg + b0 + t];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+        if (t < nb) zr[t] = x[t];
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__ probs, int nprob) {
   __shared__ __align__(16) char un[kVecLds];
   __shared__ double Ld[RNMAX], Le[RNMAX], Lc[64];
@@ -778,126 +871,15 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
   // back to classical Gram-Schmidt, twice, which any path can take.
   bool need_gs = !fast || k > 64;
   if (!need_gs) {
-    double* G = Zl + (size_t)n * ldz;  // k x k (ld 65), lower triangle, after Z (pivots no longer needed)
-    for (int pass = 0; pass < 2 && !need_gs; ++pass) {
-      // G = Z^T Z: task (i, jb) sums columns 8 jb .. 8 jb + 7 (<= i) against column i
-      const int nb8 = (k + 7) >> 3;
-      for (int task = tid; task < k * nb8; task += VNT) {
-        const int i = task / nb8, jb = task - i * nb8;
-        if (8 * jb > i) continue;
-        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int rr = 0; rr < n; ++rr) {
-          const double* zr = Zl + (size_t)rr * ldz;
-          const double zi = zr[i];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) acc[t] = fma(zi, zr[8 * jb + t < k ? 8 * jb + t : 0], acc[t]);
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-          if (8 * jb + t <= i) G[i * 65 + 8 * jb + t] = acc[t];
-      }
-      __syncthreads();
-      if (!chol_wg(G, 65, k)) { need_gs = true; break; }
-      // Z[r][:] <- Z[r][:] L^-T: forward substitution along the row
-      for (int rr = tid; rr < n; rr += VNT) {
-        double* zr = Zl + (size_t)rr * ldz;
-        for (int jj = 0; jj < k; ++jj) {
-          double acc = zr[jj];
-          for (int i = 0; i < jj; ++i) acc = fma(-zr[i], G[jj * 65 + i], acc);
-          zr[jj] = acc / G[jj * 65 + jj];
-        }
-      }
-      __syncthreads();
-    }
+    // Z in LDS (ld k + 1), G (ld 65) after it (the pivots are no longer needed)
+    for (int pass = 0; pass < 2 && !need_gs; ++pass)
+      if (!cholqr_pass(Zl, ldz, n, k, Zl + (size_t)n * ldz, 65)) need_gs = true;
   }
   if (need_gs && !fast && k <= 128 && n <= kBtRows) {
-    // CholeskyQR2 with Z (ld n) in global memory: G (ld k + 1) fills the LDS region,
-    // rows of Z are staged behind it RB at a time; the same formulas and summation
-    // orders as the fast path, the row solve blocked by 16 columns in registers
+    // Z (ld n) in global memory, G (ld k + 1) fills the LDS region
     need_gs = false;
-    const int ldg = k + 1;
-    double* G = (double*)un;
-    double* Zs = G + (size_t)k * ldg;
-    const int room = int((size_t(kVecLds) / 8 - (size_t)k * ldg) / size_t(k));
-    const int RB = room < 16 ? room : 16;
-    const int nb8 = (k + 7) >> 3, ntask = k * nb8;
-    constexpr int TPT = (128 * 16 + VNT - 1) / VNT;  // tasks per thread at k = 128
-    for (int pass = 0; pass < 2 && !need_gs; ++pass) {
-      double acc[TPT][8];
-#pragma unroll
-      for (int q = 0; q < TPT; ++q)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[q][t] = 0.0;
-      for (int r0 = 0; r0 < n; r0 += RB) {
-        const int nr = n - r0 < RB ? n - r0 : RB;
-        __syncthreads();
-        for (int e = tid; e < nr * k; e += VNT) {
-          const int rr = e / k, c = e - rr * k;
-          Zs[rr * k + c] = Z[(size_t)(r0 + rr) * n + c];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-          const int task = tid + q * VNT;
-          const int i = task / nb8, jb = task - i * nb8;
-          if (task >= ntask || 8 * jb > i) continue;
-          for (int rr = 0; rr < nr; ++rr) {
-            const double* zr = Zs + rr * k;
-            const double zi = zr[i];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) acc[q][t] = fma(zi, zr[8 * jb + t < k ? 8 * jb + t : 0], acc[q][t]);
-          }
-        }
-      }
-      __syncthreads();  // staging done: G may overwrite nothing it still needs (disjoint), order the writes
-#pragma unroll
-      for (int q = 0; q < TPT; ++q) {
-        const int task = tid + q * VNT;
-        const int i = task / nb8, jb = task - i * nb8;
-        if (task >= ntask || 8 * jb > i) continue;
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-          if (8 * jb + t <= i) G[i * ldg + 8 * jb + t] = acc[q][t];
-      }
-      __syncthreads();
-      STAMP(5);
-      const bool ok = chol_wg(G, ldg, k);
-      STAMP(6);
-      if (!ok) { need_gs = true; break; }
-      // Z[r][:] <- Z[r][:] L^-T, one row per thread, 16 columns at a time in registers
-      for (int rr = tid; rr < n; rr += VNT) {
-        double* zr = Z + (size_t)rr * n;
-        for (int b0 = 0; b0 < k; b0 += 16) {
-          double x[16];
-#pragma unroll
-          for (int t = 0; t < 16; ++t) x[t] = b0 + t < k ? zr[b0 + t] : 0.0;
-          // the solved part of the row, 8 loads in flight per group (b0 is a multiple of 16)
-          for (int i = 0; i < b0; i += 8) {
-            double zv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) zv[u] = zr[i + u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-#pragma unroll
-              for (int t = 0; t < 16; ++t)
-                if (b0 + t < k) x[t] = fma(-zv[u], G[(b0 + t) * ldg + i + u], x[t]);
-          }
-#pragma unroll
-          for (int t = 0; t < 16; ++t) {
-            if (b0 + t < k) {
-#pragma unroll
-              for (int s2 = 0; s2 < t; ++s2) x[t] = fma(-x[s2], G[(b0 + t) * ldg + b0 + s2], x[t]);
-              x[t] = x[t] / G[(b0 + t) * ldg + b0 + t];
-            }
-          }
-#pragma unroll
-          for (int t = 0; t < 16; ++t)
-            if (b0 + t < k) zr[b0 + t] = x[t];
-        }
-      }
-      __syncthreads();
-      STAMP(7);
-    }
+    for (int pass = 0; pass < 2 && !need_gs; ++pass)
+      if (!cholqr_pass(Z, n, n, k, (double*)un, k + 1)) need_gs = true;
   }
   if (need_gs) {
     // classical Gram-Schmidt, twice, descending; dots split over 8 row chunks
@@ -939,7 +921,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
   STAMP(1);
   if (!fast && n <= kBtRows) {  // U = Q D Z by k_heev_bt
 #ifdef HBM_STAMP
-    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu (gram %llu chol %llu solve %llu) gs %d\n", n, k, stamp_acc[0], stamp_acc[1], stamp_acc[5], stamp_acc[6], stamp_acc[7], int(need_gs));
+    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu gs %d\n", n, k, stamp_acc[0], stamp_acc[1], int(need_gs));
 #endif
     return;
   }
