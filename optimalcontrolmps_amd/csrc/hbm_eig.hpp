@@ -689,29 +689,109 @@ __device__ __forceinline__ T block_sum_r(T v, T* red) {
   return s;
 }
 
-// Right-looking Cholesky G = L L^T of the lower triangle of G (order k, ld
-// ldg, LDS) by the whole workgroup: per column, every thread reads the pivot,
-// threads over rows scale the column, a barrier, then waves over rows and
-// lanes over columns apply the rank-1 update (and one thread stores the
-// diagonal, which nothing reads until the next column), a barrier.  The same
-// operations in the same order per element as a one-wave Cholesky, with two
-// barriers per column instead of k dependent LDS round trips.  false
-// (uniform): a pivot <= 1e-10 (the columns are unit vectors: a near
-// dependency).  Caller: barrier before (G written), none needed after.
+// lane l's value of v (l uniform)
+__device__ __forceinline__ double rdl(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(unsigned long long)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Blocked right-looking Cholesky G = L L^T of the lower triangle of G
+// (order k <= 128, ld ldg, LDS) by the workgroup, 16 columns per block: wave 0
+// factors the block's panel (rows b0..k-1) in registers, a barrier, then the trailing lower triangle takes the block's
+// rank-16 update on the matrix cores (16 x 16 tiles over the waves; lane l
+// holds L[row 16 I + (l & 15)][b0 + kk] and L[col 16 J + (l & 15)][b0 + kk],
+// kk = 4 s + (l >> 4)), a barrier.  false (uniform): a pivot <= 1e-10 (the
+// columns are unit vectors: a near dependency).  Caller: barrier before (G
+// written), none needed after.
 __device__ __forceinline__ bool chol_wg(double* G, int ldg, int k) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  for (int cc = 0; cc < k; ++cc) {
-    const double dgg = G[cc * ldg + cc];
-    if (!(dgg > 1e-10)) return false;
-    const double dd = sqrt(dgg);
-    for (int i = cc + 1 + tid; i < k; i += VNT) G[i * ldg + cc] = G[i * ldg + cc] / dd;
-    __syncthreads();
-    if (tid == 0) G[cc * ldg + cc] = dd;
-    for (int i = cc + 1 + wv; i < k; i += VNT / 64) {
-      const double li = G[i * ldg + cc];
-      for (int jj = cc + 1 + lane; jj <= i; jj += 64) G[i * ldg + jj] = fma(-li, G[jj * ldg + cc], G[i * ldg + jj]);
+  const int a16 = lane & 15, kq = lane >> 4;
+  __shared__ int chol_bad;
+  for (int b0 = 0; b0 < k; b0 += 16) {
+    const int be = b0 + 16 < k ? b0 + 16 : k;
+    if (wv == 0) {
+      // the panel in registers: lane holds rows lane and lane + 64 of its 16 columns;
+      // column c's pivot and the entries L[b0 + c2][b0 + c] come by readlane
+      int bad = 0;
+      double pr[2][16];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int row = lane + 64 * h;
+          pr[h][c] = (row < k && b0 + c < be && b0 + c <= row) ? G[row * ldg + b0 + c] : 0.0;
+        }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int cc = b0 + c;
+        if (cc < be && !bad) {  // uniform; no break: every register index stays static
+          const double dgg = rdl(cc < 64 ? pr[0][c] : pr[1][c], cc & 63);
+          if (!(dgg > 1e-10)) {
+            bad = 1;
+          } else {
+            const double dd = sqrt(dgg), inv = 1.0 / dd;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int row = lane + 64 * h;
+              pr[h][c] = row > cc ? pr[h][c] * inv : (row == cc ? dd : pr[h][c]);
+            }
+#pragma unroll
+            for (int c2 = c + 1; c2 < 16; ++c2) {
+              const int j = b0 + c2;
+              if (j < be) {
+                const double ljc = rdl(j < 64 ? pr[0][c] : pr[1][c], j & 63);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                  const int row = lane + 64 * h;
+                  if (row >= j) pr[h][c2] = fma(-pr[h][c], ljc, pr[h][c2]);
+                }
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int row = lane + 64 * h;
+          if (row < k && b0 + c < be && b0 + c <= row) G[row * ldg + b0 + c] = pr[h][c];
+        }
+      if (lane == 0) chol_bad = bad;
     }
     __syncthreads();
+    if (chol_bad) return false;
+    const int m = k - be;
+    if (m > 0) {
+      const int T = (m + 15) >> 4, ntile = T * (T + 1) / 2, nb = be - b0;
+      for (int t = wv; t < ntile; t += VNT / 64) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        const int ra = be + 16 * I + a16, cb = be + 16 * J + a16;
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = be + 16 * I + kq + 4 * r;
+          acc[r] = (row < k && cb < k) ? G[row * ldg + cb] : 0.0;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int kk = 4 * s + kq;
+          const double va = (ra < k && kk < nb) ? -G[ra * ldg + b0 + kk] : 0.0;
+          const double vb = (cb < k && kk < nb) ? G[cb * ldg + b0 + kk] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = be + 16 * I + kq + 4 * r;
+          if (row < k && cb < k && cb <= row) G[row * ldg + cb] = acc[r];
+        }
+      }
+      __syncthreads();
+    }
   }
   return true;
 }
@@ -725,9 +805,27 @@ __device__ __forceinline__ bool chol_wg(double* G, int ldg, int k) {
 // Z_B -= Z_{<B} L_{B,<B}^T (waves over 16-row tiles), then every row's
 // 16 x 16 forward substitution against L_BB by one thread.  false (uniform):
 // a collapsed pivot (Z untouched by this pass).  Caller: barrier before.
+#ifdef HBM_STAMP
+__device__ unsigned long long g_cq_st[4];  // gram, chol, block updates, row substitutions (block 0, thread 0)
+#define CQ_STAMP(slot)                                                               \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long t_;                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_cq_st[slot] += t_ - cq_last;          \
+    cq_last = t_;                                                                    \
+  } while (0)
+#else
+#define CQ_STAMP(slot) do {} while (0)
+#endif
 __device__ __forceinline__ bool cholqr_pass(double* Z, int ldz, int n, int k, double* G, int ldg) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int a16 = lane & 15, kq = lane >> 4;
+#ifdef HBM_STAMP
+  unsigned long long cq_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(cq_last)::"memory");
+#endif
   {
     const int T = (k + 15) >> 4, ntile = T * (T + 1) / 2;
     for (int t = wv; t < ntile; t += VNT / 64) {
@@ -755,7 +853,9 @@ __device__ __forceinline__ bool cholqr_pass(double* Z, int ldz, int n, int k, do
     }
   }
   __syncthreads();
+  CQ_STAMP(0);
   const bool ok = chol_wg(G, ldg, k);
+  CQ_STAMP(1);
   if (!ok) return false;
   for (int b0 = 0; b0 < k; b0 += 16) {
     const int nb = k - b0 < 16 ? k - b0 : 16;
@@ -787,6 +887,7 @@ __device__ __forceinline__ bool cholqr_pass(double* Z, int ldz, int n, int k, do
       }
       __syncthreads();
     }
+    CQ_STAMP(2);
     for (int rr = tid; rr < n; rr += VNT) {
       double* zr = Z + (size_t)rr * ldz + b0;
       double x[16];
@@ -805,6 +906,7 @@ __device__ __forceinline__ bool cholqr_pass(double* Z, int ldz, int n, int k, do
         if (t < nb) zr[t] = x[t];
     }
     __syncthreads();
+    CQ_STAMP(3);
   }
   return true;
 }
@@ -921,7 +1023,7 @@ __global__ __launch_bounds__(VNT) void k_heev_vecs_reg(const EProb* __restrict__
   STAMP(1);
   if (!fast && n <= kBtRows) {  // U = Q D Z by k_heev_bt
 #ifdef HBM_STAMP
-    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu gs %d\n", n, k, stamp_acc[0], stamp_acc[1], int(need_gs));
+    if (tid == 0 && blockIdx.x == 0) printf("vecs slow n=%d k=%d stamps: invit %llu orth %llu (gram %llu chol %llu blk %llu subst %llu) gs %d\n", n, k, stamp_acc[0], stamp_acc[1], g_cq_st[0], g_cq_st[1], g_cq_st[2], g_cq_st[3], int(need_gs));
 #endif
     return;
   }
