@@ -196,10 +196,20 @@ struct Engine {
   long gs_launch_hist[6] = {0};
   double gs_ms[6] = {0}, gs_bflop[6] = {0}, gs_ntask[6] = {0}, gs_nseg[6] = {0}, gs_m[6] = {0}, gs_n[6] = {0}, gs_k[6] = {0};
   std::vector<int> gs_evb;  // bucket of each pending gemm_ev pair
+  // OCG_GEMM_STATS: eigensolver stream time (Gram done -> eigenvectors queued) of gauge moves
+  // (cutoff <= 1e-13, no Maxm) and of the other decompositions
+  struct EigEv { hipEvent_t a, b; int gauge; };
+  std::vector<EigEv> eig_ev;
+  double eig_ms[2] = {0, 0};
+  long eig_calls[2] = {0, 0};
   static int gs_bucket(double x) { return x < 32 ? 0 : x < 64 ? 1 : x < 128 ? 2 : x < 256 ? 3 : x < 512 ? 4 : 5; }
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gemm_ev;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_kept = nullptr;
+  // certified gauge moves (fast_certify / fast_factors); OCG_HBM_FASTGAUGE=0: eigen path only
+  bool fast_gauge = !(std::getenv("OCG_HBM_FASTGAUGE") && std::getenv("OCG_HBM_FASTGAUGE")[0] == '0');
+  DBuf<z> eye;  // kCholMax x kCholMax identity (ld kCholMax)
+  long fast_moves[2] = {0, 0};  // certified / fell back to the eigen path (OCG_GEMM_STATS)
   // side stream: the blocked large-order eigenvalue kernel runs beside the other blocks' kernel
   hipStream_t st2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -241,6 +251,9 @@ struct Engine {
                        gs_n[b] / gs_ntask[b], gs_k[b] / std::max(gs_nseg[b], 1.0));
     }
     if (gstat) {
+      std::fprintf(stderr, "[eig] stream ms: gauge moves %.1f (%ld calls), other decompositions %.1f (%ld calls); "
+                   "certified gauge moves %ld, fell back %ld\n",
+                   eig_ms[1], eig_calls[1], eig_ms[0], eig_calls[0], fast_moves[0], fast_moves[1]);
       long tot = 0;
       for (long v : eig_hist) tot += v;
       std::fprintf(stderr, "[eig] Gram blocks %ld by order:", tot);
@@ -266,6 +279,12 @@ struct Engine {
     thost.pinned = true;
     HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
+    {
+      std::vector<z> I(size_t(kCholMax) * kCholMax, mk(0, 0));
+      for (int i = 0; i < kCholMax; ++i) I[size_t(i) * kCholMax + i] = mk(1, 0);
+      eye.reserve(I.size());
+      HCK(hipMemcpy(eye.p, I.data(), sizeof(z) * I.size(), hipMemcpyHostToDevice));
+    }
     md = md_in;
     mdz = mdz_in;
     gate_i1 = gates;
@@ -518,6 +537,14 @@ struct Engine {
     return e;
   }
   void resolve_timers() {
+    for (auto& e : eig_ev) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) eig_ms[e.gauge] += ms;
+      ++eig_calls[e.gauge];
+      ev_pool.push_back(e.a);
+      ev_pool.push_back(e.b);
+    }
+    eig_ev.clear();
     for (size_t i = 0; i < gemm_ev.size(); ++i) {
       auto& pr = gemm_ev[i];
       float ms = 0;
@@ -762,6 +789,11 @@ struct Engine {
       return;
     }
     gemm(gt, gs);
+    hipEvent_t eva = nullptr;
+    if (gstat) {
+      eva = get_event();
+      HCK(hipEventRecord(eva, st));
+    }
     // OCG_HBM_THRESH: Maxm boundary first (k_heev_thresh), then only the
     // eigenvalues above it (k_heev_bisect) for the register-path sectors of
     // decompositions in which Maxm can bind
@@ -864,6 +896,12 @@ struct Engine {
         HCK(hipGetLastError());
       }
     }
+    if (gstat) {
+      hipEvent_t evb = get_event();
+      HCK(hipEventRecord(evb, st));
+      const int gauge = jobs[0].cutoff <= 1e-13 && jobs[0].maxm >= kNoMaxm ? 1 : 0;
+      eig_ev.push_back({eva, evb, gauge});
+    }
     HCK(hipEventSynchronize(ev_kept));
     for (size_t j = 0; j < jobs.size(); ++j) {
       jobs[j].kept.assign(Q1, 0);
@@ -939,6 +977,249 @@ struct Engine {
     }
     copy(ct);
     gemm(gt, gs);
+  }
+
+  // ------------------------------------------------------------ certified gauge moves
+  // A gauge move keeps every Gram eigenvalue when the smallest exceeds
+  // 10 x cutoff x total (hbm_eig.hpp, k_chol_cert); then it is factored by
+  // CholeskyQR2 of the tall orientation T of each sector block M (R x C):
+  //   Fromleft  (orthonormal X): R <= C: X = I, Y = M;  else T = M:
+  //             X1 = M R1^-1, X = X1 R2^-1, Y = R2 R1
+  //   Fromright (orthonormal rows Y): C <= R: Y = I, X = M;  else T = M^H:
+  //             Q1 = M^H R1^-1, Q = Q1 R2^-1, Y = Q^H, X = (R2 R1)^H
+  // with R1 from the Gram block on the small side (G1 = T^H T) and R2 from
+  // G2 = T1^H T1 of the first pass.  Same state and bond dims as the eigen
+  // path, a different (unobservable) gauge.
+  struct FastRun {
+    std::vector<int> job_p0, prob_q;
+    std::vector<CholProb> probs;
+    double* d_res = nullptr;
+    std::vector<double> h_res;
+  };
+  // Gram block of sector q of M into G (n x n): rows side M M^H if R <= C, else M^H M
+  void gram_tasks(const QMat& M, int q, z* G, std::vector<GTask>& gt, std::vector<GSeg>& gs) {
+    const int Rq = M.R[q], Cq = M.C[q], n = std::min(Rq, Cq);
+    const auto& SG = M.segs[q];
+    if (Rq <= Cq) {
+      const int s0 = int(gs.size());
+      for (auto& sg : SG) gs.push_back(gseg(sg.ptr, sg.ld, sg.ptr, sg.ld, sg.nc, 2));
+      gt.push_back(gtask(G, n, n, n, s0, int(SG.size())));
+    } else {
+      for (auto& a : SG)
+        for (auto& b : SG) {
+          const int s0 = int(gs.size());
+          gs.push_back(gseg(a.ptr, a.ld, b.ptr, b.ld, Rq, 1));
+          gt.push_back(gtask(G + size_t(a.c0) * n + b.c0, n, a.nc, b.nc, s0, 1));
+        }
+    }
+  }
+  // Cholesky factors of the problems' blocks, results read back to the host
+  void chol_run(std::vector<CholProb>& probs, std::vector<double>& h_res, double* d_res) {
+    hipLaunchKernelGGL(k_chol_cert, dim3(int(probs.size())), dim3(NT), 0, st, upload(probs));
+    HCK(hipGetLastError());
+    h_res.assign(2 * probs.size(), 0.0);
+    HCK(hipMemcpyAsync(h_res.data(), d_res, sizeof(double) * h_res.size(), hipMemcpyDeviceToHost, st));
+    HCK(hipEventRecord(ev_kept, st));
+    HCK(hipEventSynchronize(ev_kept));
+  }
+  // per job: certified (kept = full rank per sector, F holds R1 / R1^-1) or
+  // not (nothing of it changed: the eigen path).  Decided per chain from its
+  // own blocks, so every batching takes the same path for it.
+  std::vector<char> fast_certify(std::vector<DecompJob>& jobs, FastRun& F) {
+    std::vector<char> ok(jobs.size(), 0);
+    F.job_p0.assign(jobs.size() + 1, 0);
+    F.prob_q.clear();
+    F.probs.clear();
+    int np = 0;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      F.job_p0[j] = np;
+      bool fits = true;
+      int nj = 0;
+      for (int q = 0; q < Q1; ++q) {
+        const int Rq = jobs[j].M.R[q], Cq = jobs[j].M.C[q];
+        if (Rq <= 0 || Cq <= 0) continue;
+        if (std::min(Rq, Cq) > kCholMax || std::min(Rq, Cq) > jobs[j].bound[q]) fits = false;
+        ++nj;
+      }
+      ok[j] = fits && nj > 0;
+      if (ok[j]) np += nj;
+    }
+    F.job_p0[jobs.size()] = np;
+    if (np == 0) return ok;
+    F.d_res = walloc<double>(2 * size_t(np));
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      if (!ok[j]) continue;
+      for (int q = 0; q < Q1; ++q) {
+        const int Rq = jobs[j].M.R[q], Cq = jobs[j].M.C[q];
+        if (Rq <= 0 || Cq <= 0) continue;
+        const int n = std::min(Rq, Cq);
+        CholProb P{};
+        P.n = n;
+        P.G = walloc<z>(size_t(n) * n);
+        P.R = walloc<z>(size_t(n) * n);
+        P.Ri = walloc<z>(size_t(n) * n);
+        P.res = F.d_res + 2 * F.probs.size();
+        gram_tasks(jobs[j].M, q, const_cast<z*>(P.G), gt, gs);
+        F.probs.push_back(P);
+        F.prob_q.push_back(q);
+      }
+    }
+    gemm(gt, gs);
+    chol_run(F.probs, F.h_res, F.d_res);
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      if (!ok[j]) continue;
+      double total = 0;
+      for (int i = F.job_p0[j]; i < F.job_p0[j + 1]; ++i) total += F.h_res[2 * i];
+      bool c = total > 0;
+      for (int i = F.job_p0[j]; i < F.job_p0[j + 1]; ++i) {
+        const double inv2 = F.h_res[2 * i + 1];
+        if (!(inv2 > 0) || !(1.0 > 10.0 * jobs[j].cutoff * total * inv2)) c = false;
+      }
+      ok[j] = c;
+      if (!c) continue;
+      jobs[j].kept.assign(Q1, 0);
+      for (int i = F.job_p0[j]; i < F.job_p0[j + 1]; ++i) {
+        const int q = F.prob_q[i];
+        jobs[j].kept[q] = std::min(jobs[j].M.R[q], jobs[j].M.C[q]);
+      }
+    }
+    return ok;
+  }
+  // the certified jobs' factors, into the destinations decompose_factors
+  // would use.  The second pass cannot lose definiteness: the certificate
+  // bounds cond(G1) by 1e13, so T1^H T1 = I + O(1e-3).
+  void fast_factors(std::vector<DecompJob>& jobs, FastRun& F, const std::vector<char>& ok,
+                    const std::vector<std::vector<z*>>& xdst,
+                    const std::vector<std::vector<std::vector<z*>>>& ydst) {
+    std::vector<GTask> gt;
+    std::vector<GSeg> gs;
+    std::vector<CTask> ct;
+    std::vector<CholProb> p2;
+    std::vector<int> p2_of(F.probs.size(), -1);
+    std::vector<z*> T1(F.probs.size(), nullptr);
+    // pass 1: T1 = T R1^-1 (Fromleft R x n, Fromright C x n), identity sectors done
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      if (!ok[j]) continue;
+      DecompJob& J = jobs[j];
+      J.X.assign(Q1, nullptr);
+      J.Y.assign(Q1, nullptr);
+      for (int i = F.job_p0[j]; i < F.job_p0[j + 1]; ++i) {
+        const int q = F.prob_q[i], Rq = J.M.R[q], Cq = J.M.C[q], n = F.probs[i].n;
+        const auto& SG = J.M.segs[q];
+        const bool left = J.dir == kFromleft, qr = left ? Rq > Cq : Cq > Rq;
+        const bool ysplit = ydst.size() > j && !ydst[j][q].empty();
+        z* X = (xdst.size() > j && xdst[j][q]) ? xdst[j][q] : nullptr;
+        if (!qr) {
+          if (left) {  // X = I (R x R), Y = M (the site itself: ld C, intact until the flip)
+            if (!X) X = walloc<z>(size_t(Rq) * n);
+            ct.push_back(ctask(eye.p, X, Rq, Rq, kCholMax, n));
+            J.X[q] = X;
+            J.Y[q] = const_cast<z*>(SG[0].ptr);
+          } else {  // Y = I (C x C) by column segments, X = M (R x C, ld C)
+            if (!X) X = walloc<z>(size_t(Rq) * n);
+            z* Ys = ysplit ? nullptr : walloc<z>(size_t(n) * Cq);
+            for (size_t sI = 0; sI < SG.size(); ++sI) {
+              const int ld = ysplit ? SG[sI].nc : Cq;
+              z* Yd = ysplit ? ydst[j][q][sI] : Ys + SG[sI].c0;
+              ct.push_back(ctask(eye.p + SG[sI].c0, Yd, n, SG[sI].nc, kCholMax, ld));
+              ct.push_back(ctask(SG[sI].ptr, X + SG[sI].c0, Rq, SG[sI].nc, SG[sI].ld, n));
+            }
+            J.X[q] = X;
+            J.Y[q] = Ys;
+          }
+          continue;
+        }
+        const int m = left ? Rq : Cq;
+        z* t1 = walloc<z>(size_t(m) * n);
+        T1[i] = t1;
+        if (left) {
+          const int s0 = int(gs.size());
+          gs.push_back(gseg(SG[0].ptr, SG[0].ld, F.probs[i].Ri, n, Cq, 0));
+          gt.push_back(gtask(t1, n, Rq, n, s0, 1));
+        } else {
+          for (auto& sg : SG) {
+            const int s0 = int(gs.size());
+            gs.push_back(gseg(sg.ptr, sg.ld, F.probs[i].Ri, n, Rq, 1));
+            gt.push_back(gtask(t1 + size_t(sg.c0) * n, n, sg.nc, n, s0, 1));
+          }
+        }
+        CholProb P2{};
+        P2.n = n;
+        P2.G = walloc<z>(size_t(n) * n);
+        P2.R = walloc<z>(size_t(n) * n);
+        P2.Ri = walloc<z>(size_t(n) * n);
+        p2_of[i] = int(p2.size());
+        p2.push_back(P2);
+      }
+    }
+    copy(ct);
+    gemm(gt, gs);
+    gs.clear();
+    // pass 2: G2 = T1^H T1, R2, R2^-1
+    if (!p2.empty()) {
+      double* d_res2 = walloc<double>(2 * p2.size());
+      for (size_t t = 0; t < p2.size(); ++t) p2[t].res = d_res2 + 2 * t;
+      for (size_t i = 0; i < F.probs.size(); ++i) {
+        if (p2_of[i] < 0) continue;  // (problems of uncertified jobs have none)
+        const CholProb& P2 = p2[p2_of[i]];
+        int jj = 0;
+        while (F.job_p0[jj + 1] <= int(i)) ++jj;
+        const int q = F.prob_q[i];
+        const int m = jobs[jj].dir == kFromleft ? jobs[jj].M.R[q] : jobs[jj].M.C[q];
+        const int s0 = int(gs.size());
+        gs.push_back(gseg(T1[i], P2.n, T1[i], P2.n, m, 1));
+        gt.push_back(gtask(const_cast<z*>(P2.G), P2.n, P2.n, P2.n, s0, 1));
+      }
+      gemm(gt, gs);
+      gs.clear();
+      // (no readback: the second pass cannot fail, see above)
+      hipLaunchKernelGGL(k_chol_cert, dim3(int(p2.size())), dim3(NT), 0, st, upload(p2));
+      HCK(hipGetLastError());
+      // factors
+      for (size_t j = 0; j < jobs.size(); ++j) {
+        if (!ok[j]) continue;
+        DecompJob& J = jobs[j];
+        for (int i = F.job_p0[j]; i < F.job_p0[j + 1]; ++i) {
+          if (p2_of[i] < 0) continue;
+          const CholProb& P1 = F.probs[i];
+          const CholProb& P2 = p2[p2_of[i]];
+          const int q = F.prob_q[i], Rq = J.M.R[q], Cq = J.M.C[q], n = P1.n;
+          const auto& SG = J.M.segs[q];
+          z* X = (xdst.size() > j && xdst[j][q]) ? xdst[j][q] : walloc<z>(size_t(Rq) * n);
+          J.X[q] = X;
+          if (J.dir == kFromleft) {  // X = T1 R2^-1 (R x n), Y = R2 R1 (n x n = C)
+            int s0 = int(gs.size());
+            gs.push_back(gseg(T1[i], n, P2.Ri, n, n, 0));
+            gt.push_back(gtask(X, n, Rq, n, s0, 1));
+            z* Ys = walloc<z>(size_t(n) * Cq);
+            s0 = int(gs.size());
+            gs.push_back(gseg(P2.R, n, P1.R, n, n, 0));
+            gt.push_back(gtask(Ys, Cq, n, n, s0, 1));
+            J.Y[q] = Ys;
+          } else {  // Q = T1 R2^-1 (C x n), Y = Q^H by column segments, X = R1^H R2^H (n x n = R)
+            z* Q = walloc<z>(size_t(Cq) * n);
+            int s0 = int(gs.size());
+            gs.push_back(gseg(T1[i], n, P2.Ri, n, n, 0));
+            gt.push_back(gtask(Q, n, Cq, n, s0, 1));
+            s0 = int(gs.size());
+            gs.push_back(gseg(P1.R, n, P2.R, n, n, 3));
+            gt.push_back(gtask(X, n, n, n, s0, 1));
+            const bool ysplit = ydst.size() > j && !ydst[j][q].empty();
+            z* Ys = ysplit ? nullptr : walloc<z>(size_t(n) * Cq);
+            for (size_t sI = 0; sI < SG.size(); ++sI) {
+              const int ld = ysplit ? SG[sI].nc : Cq;
+              z* Yd = ysplit ? ydst[j][q][sI] : Ys + SG[sI].c0;
+              ct.push_back(ctask(Q + size_t(SG[sI].c0) * n, Yd, n, SG[sI].nc, n, ld, 1));
+            }
+            J.Y[q] = Ys;
+          }
+        }
+      }
+      gemm(gt, gs);
+      copy(ct);
+    }
   }
 
   // denmatDecomp(M, A, B, Fromleft, {Cutoff, Maxm}) of nm independent dense
@@ -1030,6 +1311,47 @@ struct Engine {
   const int* bound_row(int b, bool zip) const { return (zip ? mdz.data() : md.data()) + size_t(b) * Q1; }
 
   // ------------------------------------------------------------ gauge moves
+  // Decomposition of a batch of gauge-move jobs: the certified ones (fast_*,
+  // when the move qualifies) and the eigen path for the others, each chain's
+  // path decided from its own blocks.  layout(): the caller's destinations
+  // from jobs[].kept, called once every kept count is known.
+  template <class Layout>
+  void decompose_gauge(std::vector<DecompJob>& jobs, double cut, int mm, const std::vector<std::vector<z*>>& xdst,
+                       const std::vector<std::vector<std::vector<z*>>>& ydst, Layout layout) {
+    std::vector<char> ok(jobs.size(), 0);
+    FastRun F;
+    if (fast_gauge && cut <= 1e-13 && mm >= kNoMaxm) ok = fast_certify(jobs, F);
+    std::vector<int> eidx;
+    for (size_t j = 0; j < jobs.size(); ++j)
+      if (!ok[j]) eidx.push_back(int(j));
+    if (gstat && fast_gauge && cut <= 1e-13 && mm >= kNoMaxm) {
+      fast_moves[0] += long(jobs.size() - eidx.size());
+      fast_moves[1] += long(eidx.size());
+    }
+    std::vector<DecompJob> sub;
+    EigRun R;
+    if (!eidx.empty()) {
+      sub.reserve(eidx.size());
+      for (int j : eidx) sub.push_back(jobs[j]);
+      decompose_eig(sub, R);
+      for (size_t t = 0; t < eidx.size(); ++t) jobs[eidx[t]].kept = sub[t].kept;
+    }
+    layout();
+    if (eidx.size() < jobs.size()) fast_factors(jobs, F, ok, xdst, ydst);
+    if (!eidx.empty()) {
+      std::vector<std::vector<z*>> xs;
+      std::vector<std::vector<std::vector<z*>>> ys;
+      for (int j : eidx) {
+        if (!xdst.empty()) xs.push_back(xdst[j]);
+        if (!ydst.empty()) ys.push_back(ydst[j]);
+      }
+      decompose_factors(sub, R, xs, ys);
+      for (size_t t = 0; t < eidx.size(); ++t) {
+        jobs[eidx[t]].X = sub[t].X;
+        jobs[eidx[t]].Y = sub[t].Y;
+      }
+    }
+  }
   // MPS::position one site right / left for a batch (cutoff/maxm/normalize
   // as given; the gauge moves of doStep and exactApplyMPO use 1e-14, no Maxm).
   void move_right(std::vector<Chain*>& cs, int k, double cut, int mm, bool zip) {
@@ -1042,19 +1364,19 @@ struct Engine {
       jobs[i].normalize = 0;
       jobs[i].bound = bound_row(k, zip);
     }
-    EigRun R;
-    decompose_eig(jobs, R);
     // new bond k dims -> new layouts of sites k and k+1
     std::vector<std::vector<z*>> xdst(cs.size(), std::vector<z*>(Q1, nullptr));
     std::vector<Dims> nd(cs.size());
-    for (size_t i = 0; i < cs.size(); ++i) {
-      nd[i] = cs[i]->dims;
-      for (int q = 0; q < Q1; ++q) nd[i].at(k, q) = jobs[i].kept[q];
-      SiteLayout sl = site_layout(nd[i], k, p);
-      for (int q = 0; q < Q1; ++q)
-        if (jobs[i].kept[q] > 0 && sl.lmat[q] >= 0) xdst[i][q] = cs[i]->other(k) + sl.lmat[q];
-    }
-    decompose_factors(jobs, R, xdst, {});
+    auto layout = [&]() {
+      for (size_t i = 0; i < cs.size(); ++i) {
+        nd[i] = cs[i]->dims;
+        for (int q = 0; q < Q1; ++q) nd[i].at(k, q) = jobs[i].kept[q];
+        SiteLayout sl = site_layout(nd[i], k, p);
+        for (int q = 0; q < Q1; ++q)
+          xdst[i][q] = (jobs[i].kept[q] > 0 && sl.lmat[q] >= 0) ? cs[i]->other(k) + sl.lmat[q] : nullptr;
+      }
+    };
+    decompose_gauge(jobs, cut, mm, xdst, {}, layout);
     // site k+1 <- Y * site k+1, block by block
     std::vector<GTask> gt;
     std::vector<GSeg> gs;
@@ -1091,28 +1413,29 @@ struct Engine {
       jobs[i].normalize = 0;
       jobs[i].bound = bound_row(k - 1, zip);
     }
-    EigRun R;
-    decompose_eig(jobs, R);
     std::vector<std::vector<std::vector<z*>>> ydst(cs.size(), std::vector<std::vector<z*>>(Q1));
     std::vector<Dims> nd(cs.size());
-    for (size_t i = 0; i < cs.size(); ++i) {
-      nd[i] = cs[i]->dims;
-      for (int q = 0; q < Q1; ++q) nd[i].at(k - 1, q) = jobs[i].kept[q];
-      SiteLayout sl = site_layout(nd[i], k, p);
-      for (int q = 0; q < Q1; ++q) {
-        if (jobs[i].kept[q] <= 0) continue;
-        auto& segs = jobs[i].M.segs[q];
-        // the segments are the blocks (q, n) with both dims nonzero, in n order
-        for (int n = 0; n < p && q + n < Q1; ++n) {
-          int ld;
-          const long o = sl.blk(q, n, p, nd[i], k, &ld);
-          if (o < 0) continue;
-          ydst[i][q].push_back(cs[i]->other(k) + o);
+    auto layout = [&]() {
+      for (size_t i = 0; i < cs.size(); ++i) {
+        nd[i] = cs[i]->dims;
+        for (int q = 0; q < Q1; ++q) nd[i].at(k - 1, q) = jobs[i].kept[q];
+        SiteLayout sl = site_layout(nd[i], k, p);
+        for (int q = 0; q < Q1; ++q) {
+          ydst[i][q].clear();
+          if (jobs[i].kept[q] <= 0) continue;
+          auto& segs = jobs[i].M.segs[q];
+          // the segments are the blocks (q, n) with both dims nonzero, in n order
+          for (int n = 0; n < p && q + n < Q1; ++n) {
+            int ld;
+            const long o = sl.blk(q, n, p, nd[i], k, &ld);
+            if (o < 0) continue;
+            ydst[i][q].push_back(cs[i]->other(k) + o);
+          }
+          if (ydst[i][q].size() != segs.size()) throw Error(4, "internal: right-matricisation segment mismatch");
         }
-        if (ydst[i][q].size() != segs.size()) throw Error(4, "internal: right-matricisation segment mismatch");
       }
-    }
-    decompose_factors(jobs, R, {}, ydst);
+    };
+    decompose_gauge(jobs, cut, mm, {}, ydst, layout);
     // site k-1 <- site k-1 * X, block by block
     std::vector<GTask> gt;
     std::vector<GSeg> gs;

@@ -72,7 +72,22 @@ __device__ __forceinline__ void sturm_count4(const double* d, const double* e2, 
     if (fabs(q[t]) < pivmin) q[t] = -pivmin;
     c[t] = q[t] < 0 ? 1 : 0;
   }
-  for (int i = 1; i < n; ++i) {
+  // four steps' LDS loads issued ahead of their dependent chains
+  int i = 1;
+  for (; i + 3 < n; i += 4) {
+    double dv[4], ev[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { dv[u] = d[i + u]; ev[u] = e2[i + u - 1]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        q[t] = sturm_next(dv[u] - x[t], ev[u], q[t]);
+        if (fabs(q[t]) < pivmin) q[t] = -pivmin;
+        c[t] += q[t] < 0 ? 1 : 0;
+      }
+  }
+  for (; i < n; ++i) {
     const double di = d[i], ei = e2[i - 1];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -440,6 +455,78 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
 #ifndef HBM_NO_BISECT  // timing builds of tools/eig_bench only
   if (!P.defer) bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt);
 #endif
+}
+
+// ------------------------------------------------- certified Cholesky (gauge moves)
+// A gauge move (MPS::position: cutoff 1e-14, no Maxm) keeps every eigenvalue
+// of its Gram blocks when the smallest exceeds 10 x cutoff x total (the
+// eigen path would discard nothing), and then any factorisation with the
+// moving side orthonormal gives the same state and bond dims.  The host
+// (Engine::fast_certify / fast_factors) factors those moves by CholeskyQR2;
+// this kernel gives one Gram block's Cholesky factor G = R^H R (R upper),
+// R^-1 and the certificate inputs: trace(G) and ||R^-1||_F^2, whose inverse
+// bounds lambda_min(G) from below (||R^-1||_2 <= ||R^-1||_F).
+struct CholProb {
+  const z* G;   // n x n Hermitian (ld n)
+  z* R;         // out: upper factor, zero below (ld n)
+  z* Ri;        // out: R^-1, upper (ld n)
+  double* res;  // out: [0] trace(G), [1] ||R^-1||_F^2 or -1 (a pivot <= 0)
+  int n;
+};
+constexpr int kCholMax = 64;  // orders held in LDS (G and R^-1: 2 x 64 x 65 complex)
+// one workgroup per block: right-looking by rows of R (threads over the row,
+// a barrier, the trailing upper triangle by waves over rows and lanes over
+// columns, a barrier), then column j of R^-1 by thread j (back substitution)
+__global__ __launch_bounds__(NT) void k_chol_cert(const CholProb* __restrict__ probs) {
+  __shared__ z Gs[kCholMax][kCholMax + 1];
+  __shared__ z Rs[kCholMax][kCholMax + 1];
+  __shared__ double red[NT / 64];
+  const CholProb P = probs[blockIdx.x];
+  const int n = P.n, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  for (int e = tid; e < n * n; e += NT) {
+    const int i = e / n, j = e - i * n;
+    Gs[i][j] = P.G[e];
+  }
+  __syncthreads();
+  const double tr = block_sum(tid < n ? Gs[tid][tid].x : 0.0, red);
+  bool ok = true;
+  for (int i = 0; i < n; ++i) {
+    const double d = Gs[i][i].x;
+    if (!(d > 0)) { ok = false; break; }  // uniform
+    const double rii = sqrt(d), inv = 1.0 / rii;
+    for (int j = i + 1 + tid; j < n; j += NT) Gs[i][j] = zsc(Gs[i][j], inv);
+    __syncthreads();
+    if (tid == 0) Gs[i][i] = mk(rii, 0);
+    for (int a = i + 1 + wv; a < n; a += NT / 64) {
+      const z ra = zcj(Gs[i][a]);
+      for (int b = a + lane; b < n; b += 64) Gs[a][b] = zsub(Gs[a][b], zmul(ra, Gs[i][b]));
+    }
+    __syncthreads();
+  }
+  double inv2 = 0;
+  if (ok && tid < n) {
+    const int j = tid;
+    Rs[j][j] = mk(1.0 / Gs[j][j].x, 0);
+    inv2 = Rs[j][j].x * Rs[j][j].x;
+    for (int i = j - 1; i >= 0; --i) {
+      z acc = mk(0, 0);
+      for (int l = i + 1; l <= j; ++l) acc = zadd(acc, zmul(Gs[i][l], Rs[l][j]));
+      const z v = zsc(acc, -1.0 / Gs[i][i].x);
+      Rs[i][j] = v;
+      inv2 += v.x * v.x + v.y * v.y;
+    }
+  }
+  inv2 = block_sum(inv2, red);  // uniform ok: every thread takes the same path
+  if (!ok) {
+    if (tid == 0) { P.res[0] = tr; P.res[1] = -1.0; }
+    return;
+  }
+  for (int e = tid; e < n * n; e += NT) {
+    const int i = e / n, j = e - i * n;
+    P.R[e] = j >= i ? Gs[i][j] : mk(0, 0);
+    P.Ri[e] = j >= i ? Rs[i][j] : mk(0, 0);
+  }
+  if (tid == 0) { P.res[0] = tr; P.res[1] = inv2; }
 }
 
 // ------------------------------------------------- Maxm boundary, then bisection

@@ -117,6 +117,13 @@ int main(int argc, char** argv) {
   }
 #ifdef HBM_STAMP
   {
+    // the vals kernel alone once more (the vecs kernel reuses P.Z), then its stamps
+    CK(hipMemcpy(dA, As[0].data(), sizeof(z) * nn, hipMemcpyHostToDevice));
+    {
+      const int lds = (n >= regmin && n <= RNMAX) ? reg_lds_bytes(reg_grid(n)) : 64 * n + (n <= kLdsOrder ? 16 * n * n : 0) + 64;
+      if (n <= RNMAX) hipLaunchKernelGGL(k_heev_vals_any, dim3(1), dim3(RNT), lds, 0, dP, didx, regmin);
+      CK(hipDeviceSynchronize());
+    }
     std::vector<double> st(8);
     CK(hipMemcpy(st.data(), dZ, 64, hipMemcpyDeviceToHost));
     const char* nm[8] = {"colprep", "barA", "reflector", "barA'", "matvec", "barB/C", "combine+K", "update"};
