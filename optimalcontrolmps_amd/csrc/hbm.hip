@@ -251,6 +251,8 @@ struct Engine {
                        gs_n[b] / gs_ntask[b], gs_k[b] / std::max(gs_nseg[b], 1.0));
     }
     if (gstat) {
+      std::fprintf(stderr, "[step] host ms over %ld gates: theta+gate queued %.1f, two-site decomposition %.1f, gauge moves %.1f, "
+                   "gate sync %.1f\n", phase_n[0], phase_ms[0], phase_ms[1], phase_ms[2], phase_ms[3]);
       std::fprintf(stderr, "[eig] stream ms: gauge moves %.1f (%ld calls), other decompositions %.1f (%ld calls); "
                    "certified gauge moves %ld, fell back %ld\n",
                    eig_ms[1], eig_calls[1], eig_ms[0], eig_calls[0], fast_moves[0], fast_moves[1]);
@@ -461,13 +463,19 @@ struct Engine {
     std::vector<std::pair<char*, size_t>> blk;
     size_t bi = 0, top = 0;
     bool pinned = false;
+    bool same_va = true;  // pinned chunks: the device reads them at the host address
     char* get(size_t bytes) {
       bytes = (bytes + 255) & ~size_t(255);
       while (bi < blk.size() && top + bytes > blk[bi].second) { ++bi; top = 0; }
       if (bi == blk.size()) {
         const size_t sz = std::max<size_t>(bytes, blk.empty() ? (size_t(8) << 20) : 2 * blk.back().second);
         char* ptr = nullptr;
-        if (pinned) HCK(hipHostMalloc((void**)&ptr, sz, hipHostMallocDefault));
+        if (pinned) {
+          // coherent (not cached by the device): small task lists are read in place
+          HCK(hipHostMalloc((void**)&ptr, sz, hipHostMallocCoherent));
+          void* dp = nullptr;
+          if (hipHostGetDevicePointer(&dp, ptr, 0) != hipSuccess || dp != ptr) same_va = false;
+        }
         else HCK(hipMalloc((void**)&ptr, sz));
         blk.push_back({ptr, sz});
         top = 0;
@@ -496,13 +504,21 @@ struct Engine {
   T* walloc(size_t n) {
     return (T*)work.get(sizeof(T) * std::max<size_t>(n, 1));
   }
+  // Task lists up to zc_max bytes are read by the kernels straight from
+  // coherent pinned host memory (a few PCIe reads per workgroup) instead of
+  // a host-to-device copy, which the stream serialises as one more blit
+  // kernel before the launch; larger lists are copied.  The staging arena is
+  // recycled only after a stream synchronisation, so nothing queued can still
+  // read it.  OCG_HBM_ZC=bytes (0: always copy).
+  size_t zc_max = std::getenv("OCG_HBM_ZC") ? size_t(std::atol(std::getenv("OCG_HBM_ZC"))) : size_t(16384);
   template <class T>
   const T* upload(const std::vector<T>& v) {
     if (v.empty()) return nullptr;
     const size_t bytes = sizeof(T) * v.size();
     char* h = thost.get(bytes);
-    char* d = tdev.get(bytes);
     std::memcpy(h, v.data(), bytes);
+    if (bytes <= zc_max && thost.same_va) return (const T*)h;
+    char* d = tdev.get(bytes);
     HCK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
     return (const T*)d;
   }
@@ -515,11 +531,14 @@ struct Engine {
     const size_t ba = sizeof(A) * a.size(), bb = sizeof(B) * b.size(), bc = sizeof(C) * c.size();
     const size_t oa = 0, ob = al(ba), oc = ob + al(bb), bytes = std::max<size_t>(oc + bc, 1);
     char* h = thost.get(bytes);
-    char* d = tdev.get(bytes);
     if (ba) std::memcpy(h + oa, a.data(), ba);
     if (bb) std::memcpy(h + ob, b.data(), bb);
     if (bc) std::memcpy(h + oc, c.data(), bc);
-    HCK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    char* d = h;
+    if (!(bytes <= zc_max && thost.same_va)) {
+      d = tdev.get(bytes);
+      HCK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));
+    }
     da = ba ? (const A*)(d + oa) : nullptr;
     db = bb ? (const B*)(d + ob) : nullptr;
     dc = bc ? (const C*)(d + oc) : nullptr;
@@ -1532,26 +1551,40 @@ struct Engine {
       const int mode = fromLeft ? 0 : 1;
       const bool lonely = fromLeft && i2 == L && L % 2 == 0;  // (:153-155)
       std::vector<ThetaJob> th(B);
+      auto t0 = std::chrono::steady_clock::now();
       build_theta(cs, i1, th);
       apply_gate(cs, th, i1, uf, ut, tau, fwd, mode, lonely);
+      auto t1 = std::chrono::steady_clock::now(), t2 = t1;
       if (g + 1 < ng) {
         const int ni1 = gate_i1[g + 1], ni2 = ni1 + 1;
         if (ni1 >= i2) {
           two_site(cs, th, i1, kFromleft);
+          t2 = std::chrono::steady_clock::now();
           centre = i1 + 1;
           position(cs, centre, ni1);
         } else {
           two_site(cs, th, i1, kFromright);
+          t2 = std::chrono::steady_clock::now();
           centre = i1;
           position(cs, centre, ni2);
         }
         if (i2 == ni1 || i1 == ni2) fromLeft = false;
       } else {
         two_site(cs, th, i1, kFromright);
+        t2 = std::chrono::steady_clock::now();
         centre = i1;
         position(cs, centre, 1);
       }
+      auto t3 = std::chrono::steady_clock::now();
       sync();
+      if (gstat) {  // host wall per phase of the step (each ends at a stream synchronisation)
+        auto t4 = std::chrono::steady_clock::now();
+        phase_ms[0] += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        phase_ms[1] += std::chrono::duration<double, std::milli>(t2 - t1).count();
+        phase_ms[2] += std::chrono::duration<double, std::milli>(t3 - t2).count();
+        phase_ms[3] += std::chrono::duration<double, std::milli>(t4 - t3).count();
+        ++phase_n[0];
+      }
     }
     // U_to on site 1 (:222-223) and psi.normalize() (:228)
     std::vector<View> vs;

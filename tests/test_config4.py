@@ -97,6 +97,53 @@ def test_c4_w256_step_blocked_eigensolver(c4, warm256, monkeypatch):
     eng.close()
 
 
+@pytest.mark.parametrize("fast", ["1", "0"])
+def test_c4_w256_step_certified_gauge_moves(c4, warm256, monkeypatch, fast):
+    """Gauge moves by certified CholeskyQR2 (default, OCG_HBM_FASTGAUGE=1) or
+    by the eigen decomposition (0): the oracle's bond dimensions and overlaps
+    either way (the gauge is not observable), and the two paths' states equal
+    to rounding as MPS (overlap 1)."""
+    from optimalcontrolmps_amd.native import Engine
+    if "w256/bonds1" not in c4:
+        pytest.skip("w256 oracle fixture not generated")
+    monkeypatch.setenv("OCG_HBM_FASTGAUGE", fast)
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    psi1 = eng.steps(warm256, np.array([2.5, 3.0]), True)
+    assert list(psi1.bond_dims()) == list(c4["w256/bonds1"])
+    assert abs(eng.overlap(warm256, psi1) - complex(c4["w256/ov01"][0])) <= 1e-10
+    dh = eng.overlap(psi1, psi1, True)
+    assert abs(dh - complex(c4["w256/dH11"][0])) <= 1e-9 * abs(complex(c4["w256/dH11"][0]))
+    monkeypatch.setenv("OCG_HBM_FASTGAUGE", "0" if fast == "1" else "1")
+    other = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    psi2 = other.steps(warm256, np.array([2.5, 3.0]), True)
+    assert list(psi2.bond_dims()) == list(psi1.bond_dims())
+    assert abs(eng.overlap(psi1, psi2) - 1.0) <= 1e-11
+    eng.close()
+    other.close()
+
+
+def test_c4_s32_hessian_certified_vs_eigen_gauge(c4, monkeypatch):
+    """getHessian at config 4's chain (Maxm 32) with the certified gauge moves
+    and with the eigen path only: equal to rounding, both at the oracle
+    fixture's tolerance"""
+    from optimalcontrolmps_amd.native import Engine
+    u = c4["s32/u"]
+    Ho = c4["s32/H"]
+    out = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("OCG_HBM_FASTGAUGE", fast)
+        eng = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+        eng.set_states(_mps(c4["s32/tgt_dims"], c4["s32/tgt_data"]), _mps(c4["s32/init_dims"], c4["s32/init_data"]))
+        H, divT, F = eng.hessian(u)
+        out[fast] = (H, divT, F)
+        assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+        eng.close()
+    (H1, d1, F1), (H0, d0, F0) = out["1"], out["0"]
+    assert abs(F1 - F0) <= 1e-11
+    assert np.abs(d1 - d0).max() <= 1e-10
+    assert np.abs(H1 - H0).max() <= 1e-9 * np.abs(H0).max()
+
+
 def test_c4_w256_batched_equals_single(warm256):
     """ocg_step_batch over differently-driven chains == one ocg_step each (bitwise):
     a chain's arithmetic does not depend on what else is in the batch."""
