@@ -252,7 +252,8 @@ struct Engine {
     }
     if (gstat) {
       std::fprintf(stderr, "[step] host ms over %ld gates: theta+gate queued %.1f, two-site decomposition %.1f, gauge moves %.1f, "
-                   "gate sync %.1f\n", phase_n[0], phase_ms[0], phase_ms[1], phase_ms[2], phase_ms[3]);
+                   "gate sync %.1f; waits: certificate %.1f (%ld), eigen kept counts %.1f (%ld)\n", phase_n[0], phase_ms[0],
+                   phase_ms[1], phase_ms[2], phase_ms[3], phase_ms[4], phase_n[1], phase_ms[5], phase_n[2]);
       std::fprintf(stderr, "[eig] stream ms: gauge moves %.1f (%ld calls), other decompositions %.1f (%ld calls); "
                    "certified gauge moves %ld, fell back %ld\n",
                    eig_ms[1], eig_calls[1], eig_ms[0], eig_calls[0], fast_moves[0], fast_moves[1]);
@@ -895,8 +896,11 @@ struct Engine {
     HCK(hipGetLastError());
     R.h_kept.assign(np, 0);
     R.h_keptw.assign(2 * jobs.size(), 0.0);
-    HCK(hipMemcpyAsync(R.h_kept.data(), R.d_kept, sizeof(int) * np, hipMemcpyDeviceToHost, st));
-    HCK(hipMemcpyAsync(R.h_keptw.data(), R.d_keptw, sizeof(double) * 2 * jobs.size(), hipMemcpyDeviceToHost, st));
+    // into pinned staging (asynchronous copies; pageable memory would block here)
+    int* hk = (int*)thost.get(sizeof(int) * np);
+    double* hw = (double*)thost.get(sizeof(double) * 2 * jobs.size());
+    HCK(hipMemcpyAsync(hk, R.d_kept, sizeof(int) * np, hipMemcpyDeviceToHost, st));
+    HCK(hipMemcpyAsync(hw, R.d_keptw, sizeof(double) * 2 * jobs.size(), hipMemcpyDeviceToHost, st));
     HCK(hipEventRecord(ev_kept, st));
     // eigenvectors of the kept eigenvalues (reads the kept counts on the device)
     hipLaunchKernelGGL(k_heev_vecs_reg, dim3(np), dim3(VNT), 0, st, R.d_probs, np);
@@ -921,7 +925,14 @@ struct Engine {
       const int gauge = jobs[0].cutoff <= 1e-13 && jobs[0].maxm >= kNoMaxm ? 1 : 0;
       eig_ev.push_back({eva, evb, gauge});
     }
-    HCK(hipEventSynchronize(ev_kept));
+    {
+      const auto t0 = std::chrono::steady_clock::now();
+      HCK(hipEventSynchronize(ev_kept));
+      if (gstat) phase_ms[5] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      ++phase_n[2];
+      std::memcpy(R.h_kept.data(), hk, sizeof(int) * np);
+      std::memcpy(R.h_keptw.data(), hw, sizeof(double) * 2 * jobs.size());
+    }
     for (size_t j = 0; j < jobs.size(); ++j) {
       jobs[j].kept.assign(Q1, 0);
       for (int i = R.job_p0[j]; i < R.job_p0[j + 1]; ++i) jobs[j].kept[R.prob_q[i]] = R.h_kept[i];
@@ -1037,9 +1048,15 @@ struct Engine {
     hipLaunchKernelGGL(k_chol_cert, dim3(int(probs.size())), dim3(NT), 0, st, upload(probs));
     HCK(hipGetLastError());
     h_res.assign(2 * probs.size(), 0.0);
-    HCK(hipMemcpyAsync(h_res.data(), d_res, sizeof(double) * h_res.size(), hipMemcpyDeviceToHost, st));
+    // into pinned staging (an asynchronous copy; pageable memory would block here)
+    double* hp = (double*)thost.get(sizeof(double) * h_res.size());
+    HCK(hipMemcpyAsync(hp, d_res, sizeof(double) * h_res.size(), hipMemcpyDeviceToHost, st));
     HCK(hipEventRecord(ev_kept, st));
+    const auto t0 = std::chrono::steady_clock::now();
     HCK(hipEventSynchronize(ev_kept));
+    if (gstat) phase_ms[4] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ++phase_n[1];
+    std::memcpy(h_res.data(), hp, sizeof(double) * h_res.size());
   }
   // per job: certified (kept = full rank per sector, F holds R1 / R1^-1) or
   // not (nothing of it changed: the eigen path).  Decided per chain from its
