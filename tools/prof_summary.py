@@ -31,12 +31,13 @@ def kernel_stats(db):
 def pmc(db, counter):
     c = sqlite3.connect(db)
     out = {}
-    for name, val in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
-                               (counter,)):
+    for name, val, n in c.execute("select kernel_name, sum(value), count(*) from counters_collection "
+                                  "where counter_name = ? group by kernel_name", (counter,)):
         k = short(name)
         s = out.setdefault(k, [0.0, 0])
         s[0] += val
-        s[1] += 1
+        s[1] += n
+    print(f"  {counter}: {len(out)} kernels", flush=True)
     return out
 
 

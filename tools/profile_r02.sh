@@ -20,5 +20,11 @@ timeout -s KILL $T2 rocprofv3 --pmc FETCH_SIZE -d $D/pmc_fetch -o run -- python3
 timeout -s KILL $T2 rocprofv3 --pmc WRITE_SIZE -d $D/pmc_write -o run -- python3 $R/bench.py $ARGS > $L/pmc_write_$TAG.log 2>&1 || exit $?
 timeout -s KILL $T2 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_FMA_F64 GRBM_GUI_ACTIVE -d $D/pmc_mfma -o run -- python3 $R/bench.py $ARGS > $L/pmc_mfma_$TAG.log 2>&1 || exit $?
 grep "\"metric\"" $L/prof_$TAG.log | tail -1 | cut -c1-400
-PROF_DB_ROOT=$D python3 $R/tools/prof_summary.py $TAG $L > $L/summary_stdout.txt 2>&1
+# the summary reads large databases (config 5): a heartbeat file keeps the run visibly alive
+PROF_DB_ROOT=$D python3 -u $R/tools/prof_summary.py $TAG $L > $L/summary_stdout.txt 2>&1 &
+spid=$!
+while kill -0 $spid 2>/dev/null; do date >> $L/heartbeat.txt; sleep 30; done
+wait $spid
+src=$?
 rm -rf $D
+exit $src
