@@ -511,8 +511,12 @@ def bench_c4(args):
                           "avg_launch_ms": gemm_ms, "share_of_time": gm["ms"] / (1e3 * elapsed),
                           "achieved_tflops": gm["alg_flops"] / max(gm["ms"], 1e-9) / 1e9,
                           "achieved_gbs": gm["alg_bytes"] / max(gm["ms"], 1e-9) / 1e6},
+            # config 5: the profile of this command also covers the untimed chi=512 warm-up
+            # (single-chain launches, a different population than the timed getHessian's row
+            # batches), so its per-dispatch traffic is not this region's: traffic stays null
             "roofline": roofline_block("hbm::k_gemm", gemm_ms, gm["alg_bytes"] / max(1, gm["launches"]),
-                                       gm["alg_flops"] / max(1, gm["launches"]), tag, bound="latency",
+                                       gm["alg_flops"] / max(1, gm["launches"]), None if c5 else tag,
+                                       bound="latency",
                                        limiter="the per-sector Hermitian eigensolver (k_heev_*) sets the step time; "
                                                "k_gemm launches are small (tasks of m, n ~ 16-60) and latency-bound"),
         }
@@ -525,7 +529,10 @@ def bench_c4(args):
 def measured_traffic(kernel, tag="r01"):
     """HBM bytes per dispatch of `kernel` from the committed rocprofv3 PMC passes
     of this same command (profiles/<tag>_summary.json, written by
-    tools/prof_summary.py; FETCH_SIZE doubled per the gfx950 calibration)."""
+    tools/prof_summary.py; FETCH_SIZE doubled per the gfx950 calibration);
+    None when there is no such profile (tag None)."""
+    if tag is None:
+        return None
     try:
         with open(os.path.join(ROOT, "profiles", f"{tag}_summary.json")) as f:
             return json.load(f)["pmc_per_dispatch"][kernel]["hbm_bytes"]
