@@ -511,6 +511,8 @@ struct Engine {
   // kernel before the launch; larger lists are copied.  The staging arena is
   // recycled only after a stream synchronisation, so nothing queued can still
   // read it.  OCG_HBM_ZC=bytes (0: always copy).
+  // k_gemm's XCD-grouped tile order (OCG_HBM_XCDMAP=0: dispatch order)
+  bool xcd_map = !(std::getenv("OCG_HBM_XCDMAP") && std::getenv("OCG_HBM_XCDMAP")[0] == '0');
   size_t zc_max = std::getenv("OCG_HBM_ZC") ? size_t(std::atol(std::getenv("OCG_HBM_ZC"))) : size_t(16384);
   template <class T>
   const T* upload(const std::vector<T>& v) {
@@ -629,7 +631,7 @@ struct Engine {
     hipEvent_t a = get_event(), b = get_event();
     // start / stop events of the dispatch itself (not stream markers around it: with the
     // host building the next launch's tasks the stream idles between a marker and the kernel)
-    hipExtLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, dmap, ds);
+    hipExtLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, dmap, ds, xcd_map ? 1 : 0);
     HCK(hipGetLastError());
     gemm_ev.push_back({a, b});
     ++gemm_launches;
@@ -2580,7 +2582,13 @@ int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int
   });
 }
 
-double hbm_traj_bytes(const hbm_engine* h, int N) { return 16.0 * double(h->E->state_cap) * (3.0 * N + 6.0); }
+// bytes a call holding `slots` state slots must newly allocate: 0 when the heap
+// already has them (a previous call grew it), else the whole grown heap
+// (reserve_states copies into a new allocation beside the old one)
+static double heap_growth_bytes(const hbm_engine* h, double slots) {
+  return slots <= double(h->E->heap_slots) ? 0.0 : 16.0 * double(h->E->state_cap) * slots;
+}
+double hbm_traj_bytes(const hbm_engine* h, int N) { return heap_growth_bytes(h, 3.0 * N + 6.0); }
 
 // Checkpointed getHessian (see hbm.hpp).  Time-major row sweep: all rows of a
 // batch advance together in absolute time j (row i joins at j = i with
@@ -2911,7 +2919,7 @@ int pipe_psih_base(const hbm_engine* h, int N) { return 4 + 3 * N + 2; }
 double hbm_pipe_bytes(const hbm_engine* h, int N, const int* rows, int nrows) {
   double slots = pipe_psih_base(h, N) + N;
   for (int r = 0; r < nrows; ++r) slots += std::max(0, N - 2 - rows[r]);
-  return 16.0 * double(h->E->state_cap) * slots;
+  return heap_growth_bytes(h, slots);
 }
 
 int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,

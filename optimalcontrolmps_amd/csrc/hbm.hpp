@@ -49,7 +49,8 @@ int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int
 // Leaves no device trajectories (ocg_get_state fails afterwards).
 int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                      double* F, int K);
-// states the stored-trajectory Hessian would keep (3 N + 6) x bytes per state
+// bytes the stored-trajectory Hessian's 3 N + 6 state slots would newly allocate
+// (0 when the context's state heap already holds them)
 double hbm_traj_bytes(const hbm_engine* h, int N);
 int hbm_get_state(hbm_engine* h, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
 // kinds 0-6 as ocg_kernel_stats (HIP-event phase times); 7: the MFMA GEMM
@@ -72,5 +73,6 @@ int hbm_ground_state(hbm_engine* h, const int* dims, const double* data, double 
 // for one batched overlap pass; bit-identical to propagate + xi_dH + rows
 int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                      double* F);
-// heap bytes hbm_hessian_pipe needs (trajectories + psiH_i + row states)
+// heap bytes hbm_hessian_pipe would newly allocate for its slots (trajectories +
+// psiH_i + row states; 0 when the heap already holds them, e.g. from the last call)
 double hbm_pipe_bytes(const hbm_engine* h, int N, const int* rows, int nrows);

@@ -115,15 +115,24 @@ __device__ __forceinline__ int find_task(const T* tasks, int ntask, long long e,
 // B[k = l >> 4][l & 15]; results col = l & 15, row = (l >> 4) + 4 r).
 // (GK 32 and 64 measured slower on the config-4 mix: fewer workgroups per CU.)
 constexpr int GT = 32, GK = 16;
+// xcd != 0: workgroups b and b + 8 (which the dispatcher places on one XCD,
+// MI355X_MICROARCH.md §Workgroup dispatch) take consecutive tiles, so a task's
+// tiles share that XCD's L2 for their common operand rows / columns (speed
+// only: any bijection of workgroups onto tiles computes the same result)
 __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, const int* __restrict__ tile_task,
-                                             const GSeg* __restrict__ segs) {
+                                             const GSeg* __restrict__ segs, int xcd) {
   constexpr int EA = GT * GK / NT;  // staged elements per thread and operand
   __shared__ double Ar[GT][GK + 1], Ai[GT][GK + 1], Br[GK][GT + 1], Bi[GK][GT + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int tile = blockIdx.x;
+  if (xcd) {
+    const int nb = gridDim.x, base = nb >> 3, rem = nb & 7, x = blockIdx.x & 7;
+    tile = x * base + (x < rem ? x : rem) + (blockIdx.x >> 3);
+  }
   // tile -> task from the host's table: one dependent load instead of a binary
   // search over freshly uploaded task records (the small launches' latency)
-  const GTask T = tasks[tile_task[blockIdx.x]];
-  const int tl = blockIdx.x - T.tile0;
+  const GTask T = tasks[tile_task[tile]];
+  const int tl = tile - T.tile0;
   const int ntn = (T.n + GT - 1) / GT;
   const int m0 = (tl / ntn) * GT, n0 = (tl % ntn) * GT;
   const int wm = (wv >> 1) * 16, wn = (wv & 1) * 16;
