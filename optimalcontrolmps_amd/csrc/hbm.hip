@@ -511,6 +511,8 @@ struct Engine {
   // kernel before the launch; larger lists are copied.  The staging arena is
   // recycled only after a stream synchronisation, so nothing queued can still
   // read it.  OCG_HBM_ZC=bytes (0: always copy).
+  // Gram orders <= kSmallMax on k_heev_vals_small beside the large-order kernel (OCG_HBM_SMALL=0: one launch)
+  bool small_split = !(std::getenv("OCG_HBM_SMALL") && std::getenv("OCG_HBM_SMALL")[0] == '0');
   // k_gemm's XCD-grouped tile order (OCG_HBM_XCDMAP=0: dispatch order)
   bool xcd_map = !(std::getenv("OCG_HBM_XCDMAP") && std::getenv("OCG_HBM_XCDMAP")[0] == '0');
   size_t zc_max = std::getenv("OCG_HBM_ZC") ? size_t(std::atol(std::getenv("OCG_HBM_ZC"))) : size_t(16384);
@@ -851,22 +853,41 @@ struct Engine {
       // one launch: per block the register variant for its order (or the LDS / L2
       // kernel), largest blocks first; dynamic LDS = max over the variants present
       // orders big_min <= n <= kBigMax: the blocked reduction (k_heev_vals_big)
-      std::vector<int> order, big;
-      for (int i = 0; i < np; ++i) (R.probs[i].n >= std::max(big_min, 2) && R.probs[i].n <= kBigMax ? big : order).push_back(i);
+      // orders <= kSmallMax: k_heev_vals_small on the side stream (several workgroups per CU)
+      std::vector<int> order, big, small;
+      for (int i = 0; i < np; ++i) {
+        const int n = R.probs[i].n;
+        if (n >= std::max(big_min, 2) && n <= kBigMax) big.push_back(i);
+        else if (small_split && n <= kSmallMax) small.push_back(i);
+        else order.push_back(i);
+      }
       std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
+      std::stable_sort(small.begin(), small.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
       if (gstat)
         for (int i = 0; i < np; ++i) ++eig_hist[std::min(R.probs[i].n / 16, 33)];
       std::stable_sort(big.begin(), big.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
-      if (!big.empty()) {  // on the side stream, after everything st has queued (incl. this upload)
+      const bool side = !big.empty() || !small.empty();
+      if (side) {  // on the side stream, after everything st has queued (incl. this upload)
         if (!st2) {  // created on first use: every stream takes a hardware queue (GPU_MAX_HW_QUEUES)
           HCK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
           HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
           HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
         }
         const int* dbig = upload(big);
+        const int* dsmall = upload(small);
         HCK(hipEventRecord(ev_fork, st));
         HCK(hipStreamWaitEvent(st2, ev_fork, 0));
-        hipLaunchKernelGGL(k_heev_vals_big, dim3(int(big.size())), dim3(VBG), 0, st2, R.d_probs, dbig);
+        if (!big.empty())
+          hipLaunchKernelGGL(k_heev_vals_big, dim3(int(big.size())), dim3(VBG), 0, st2, R.d_probs, dbig);
+        if (!small.empty()) {
+          int lds_s = 64;
+          for (int i : small) {
+            const int n = R.probs[i].n;
+            lds_s = std::max(lds_s, n >= reg_min ? reg_lds_bytes(reg_grid(n)) : 64 * n + 16 * n * n + 64);
+          }
+          hipLaunchKernelGGL(k_heev_vals_small, dim3(int(small.size())), dim3(RNT), lds_s, st2, R.d_probs, dsmall,
+                             reg_min);
+        }
         HCK(hipGetLastError());
         HCK(hipEventRecord(ev_join, st2));
       }
@@ -883,14 +904,14 @@ struct Engine {
       }
       if (!thr_items.empty()) {
         // the boundary counts read every sector's tridiagonal, the blocked kernel's too
-        if (!big.empty()) HCK(hipStreamWaitEvent(st, ev_join, 0));
+        if (side) HCK(hipStreamWaitEvent(st, ev_join, 0));
         hipLaunchKernelGGL(k_heev_thresh, dim3(int(thr_items.size())), dim3(THN), thresh_lds_bytes(), st, d_items,
                            upload(thr_items), const_cast<EProb*>(R.d_probs));
         hipLaunchKernelGGL(k_heev_bisect, dim3(int(deferred.size())), dim3(BSN), bisect_lds_bytes(max_def), st,
                            R.d_probs, upload(deferred));
         HCK(hipGetLastError());
       }
-      if (!big.empty()) HCK(hipStreamWaitEvent(st, ev_join, 0));  // join before the truncation
+      if (side) HCK(hipStreamWaitEvent(st, ev_join, 0));  // join before the truncation
     }
     int maxnp = 0;
     for (auto& I : items) maxnp = std::max(maxnp, I.np);

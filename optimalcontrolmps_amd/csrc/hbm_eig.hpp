@@ -673,6 +673,25 @@ __global__ __launch_bounds__(RNT, 1) void k_heev_vals_any(const EProb* __restric
   heev_vals_lds_body(P, smem_any);
 }
 
+// Gram blocks of order <= kSmallMax: the same bodies compiled apart, so that
+// this launch's register and LDS footprint (slot grids 2 and 4, the LDS kernel)
+// lets several workgroups share a CU instead of the 512 registers per lane
+// the larger grids force on k_heev_vals_any.  Launched on the side stream
+// beside k_heev_vals_any (Engine::decompose_eig).
+constexpr int kSmallMax = 64;
+__global__ __launch_bounds__(RNT, 2) void k_heev_vals_small(const EProb* __restrict__ probs,
+                                                            const int* __restrict__ idx, int reg_min) {
+  extern __shared__ __align__(16) char smem_small[];
+  const EProb P = probs[idx[blockIdx.x]];
+  const int n = P.n;
+  if (n >= reg_min && n <= kSmallMax) {
+    if (reg_grid(n) == 2) heev_vals_reg_body<2>(P, smem_small);
+    else heev_vals_reg_body<4>(P, smem_small);
+    return;
+  }
+  heev_vals_lds_body(P, smem_small);
+}
+
 // ------------------------------------------------------------------ vectors
 // Kept eigenvectors U = Q D Z (n x k, ld k) of one problem per workgroup.
 // Fast path (n <= RNMAX, k <= 64, Z fits LDS): inverse iteration on the real
