@@ -915,7 +915,7 @@ struct Engine {
     }
     int maxnp = 0;
     for (auto& I : items) maxnp = std::max(maxnp, I.np);
-    hipLaunchKernelGGL(k_truncate, dim3(int(items.size())), dim3(NT), truncate_lds(maxnp), st, d_items, R.d_probs);
+    hipLaunchKernelGGL(k_truncate, dim3(int(items.size())), dim3(TNT), truncate_lds(maxnp), st, d_items, R.d_probs);
     HCK(hipGetLastError());
     R.h_kept.assign(np, 0);
     R.h_keptw.assign(2 * jobs.size(), 0.0);

@@ -677,7 +677,20 @@ struct TItem {
   double* keptw;    // [0] kept weight, [1] inv
 };
 constexpr int kMaxEig = 5120;  // eigenvalues of one decomposition (>= p chi for chi <= 512, p <= 9)
-__global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items, const EProb* __restrict__ probs) {
+constexpr int TNT = 1024;      // threads of k_truncate: the O(T^2) ranking spread over 16 waves
+template <class T>
+__device__ __forceinline__ T block_sum_t(T v, T* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < TNT / 64; ++i) s += red[i];
+  return s;
+}
+__global__ __launch_bounds__(TNT) void k_truncate(const TItem* __restrict__ items, const EProb* __restrict__ probs) {
   extern __shared__ __align__(16) char smem[];
   const TItem I = items[blockIdx.x];
   const int tid = threadIdx.x;
@@ -685,7 +698,7 @@ __global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items
   double* PP = LAM + kMaxEig;        // sorted descending
   int* RK = (int*)(PP + kMaxEig);    // global rank of each flat eigenvalue
   int* PO = RK + kMaxEig;            // problem offsets (np + 1)
-  __shared__ double red[NT / 64];
+  __shared__ double red[TNT / 64];
   __shared__ int sm[2];
   if (tid == 0) {
     int o = 0;
@@ -696,11 +709,11 @@ __global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items
   const int T = PO[I.np];
   for (int i = 0; i < I.np; ++i) {
     const EProb& P = probs[I.p0 + i];
-    for (int j = tid; j < P.n; j += NT) LAM[PO[i] + j] = fmax(P.w[j], 0.0);
+    for (int j = tid; j < P.n; j += TNT) LAM[PO[i] + j] = fmax(P.w[j], 0.0);
   }
   __syncthreads();
   // global rank: (lambda desc, flat index asc); problems are in sector order
-  for (int e = tid; e < T; e += NT) {
+  for (int e = tid; e < T; e += TNT) {
     const double l = LAM[e];
     int rk = 0;
     for (int f = 0; f < T; ++f) {
@@ -711,8 +724,8 @@ __global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items
     PP[rk] = l;
   }
   double tot = 0;
-  for (int e = tid; e < T; e += NT) tot += LAM[e];
-  tot = block_sum(tot, red);
+  for (int e = tid; e < T; e += TNT) tot += LAM[e];
+  tot = block_sum_t(tot, red);
   __syncthreads();
   if (tid == 0) {
     int m = T;
@@ -737,7 +750,7 @@ __global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items
   const int m = sm[0];
   // kept per sector: its eigenvalues of global rank < m (a prefix of its
   // descending list), capped by the sector's rank bound
-  for (int i = tid; i < I.np; i += NT) {
+  for (int i = tid; i < I.np; i += TNT) {
     int kq = 0;
     for (int e = PO[i]; e < PO[i + 1]; ++e) kq += RK[e] < m ? 1 : 0;
     I.kept[i] = kq < I.bound[i] ? kq : I.bound[i];
@@ -745,8 +758,8 @@ __global__ __launch_bounds__(NT) void k_truncate(const TItem* __restrict__ items
   __syncthreads();
   double kw = 0;
   for (int i = 0; i < I.np; ++i)
-    for (int j = tid; j < I.kept[i]; j += NT) kw += LAM[PO[i] + j];
-  kw = block_sum(kw, red);
+    for (int j = tid; j < I.kept[i]; j += TNT) kw += LAM[PO[i] + j];
+  kw = block_sum_t(kw, red);
   if (tid == 0) {
     I.keptw[0] = kw;
     I.keptw[1] = (I.normalize && kw > 1e-32) ? 1.0 / sqrt(kw) : 1.0;
