@@ -457,6 +457,14 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
 #endif
 }
 
+// lane l's value of v (l uniform)
+__device__ __forceinline__ double rdl(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(unsigned long long)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // ------------------------------------------------- certified Cholesky (gauge moves)
 // A gauge move (MPS::position: cutoff 1e-14, no Maxm) keeps every eigenvalue
 // of its Gram blocks when the smallest exceeds 10 x cutoff x total (the
@@ -474,13 +482,16 @@ struct CholProb {
   int n;
 };
 constexpr int kCholMax = 64;  // orders held in LDS (G and R^-1: 2 x 64 x 65 complex)
-// one workgroup per block: right-looking by rows of R (threads over the row,
-// a barrier, the trailing upper triangle by waves over rows and lanes over
-// columns, a barrier), then column j of R^-1 by thread j (back substitution)
+// one workgroup per block, blocked by 16 rows of R: wave 0 factors the
+// panel (rows b0..b0+15, lane = column b0 + lane) in registers, the pivots and
+// the entries conj(R[i][a]) coming by readlane; a barrier; the trailing upper
+// triangle takes the panel's rank-16 update (threads over elements); a
+// barrier.  Then column j of R^-1 by thread j (back substitution).
 __global__ __launch_bounds__(NT) void k_chol_cert(const CholProb* __restrict__ probs) {
   __shared__ z Gs[kCholMax][kCholMax + 1];
   __shared__ z Rs[kCholMax][kCholMax + 1];
   __shared__ double red[NT / 64];
+  __shared__ int sbad;
   const CholProb P = probs[blockIdx.x];
   const int n = P.n, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   for (int e = tid; e < n * n; e += NT) {
@@ -490,30 +501,88 @@ __global__ __launch_bounds__(NT) void k_chol_cert(const CholProb* __restrict__ p
   __syncthreads();
   const double tr = block_sum(tid < n ? Gs[tid][tid].x : 0.0, red);
   bool ok = true;
-  for (int i = 0; i < n; ++i) {
-    const double d = Gs[i][i].x;
-    if (!(d > 0)) { ok = false; break; }  // uniform
-    const double rii = sqrt(d), inv = 1.0 / rii;
-    for (int j = i + 1 + tid; j < n; j += NT) Gs[i][j] = zsc(Gs[i][j], inv);
+  for (int b0 = 0; b0 < n; b0 += 16) {
+    const int be = b0 + 16 < n ? b0 + 16 : n;
+    if (wv == 0) {
+      const int col = b0 + lane;  // n - b0 <= 64 columns from b0 on
+      const bool lv = col < n;
+      z pr[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int row = b0 + c;
+        pr[c] = (lv && row < be && col >= row) ? Gs[row][col] : mk(0, 0);
+      }
+      int pbad = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int i = b0 + c;
+        if (i < be && !pbad) {  // uniform
+          const double d = rdl(pr[c].x, c);  // lane c holds column i: its row-i entry
+          if (!(d > 0)) {
+            pbad = 1;
+          } else {
+            const double rii = sqrt(d), inv = 1.0 / rii;
+            if (col > i) pr[c] = zsc(pr[c], inv);
+            else if (col == i) pr[c] = mk(rii, 0);
+#pragma unroll
+            for (int c2 = c + 1; c2 < 16; ++c2) {
+              const int a = b0 + c2;
+              if (a < be) {  // G[a][b] -= conj(R[i][a]) R[i][b], b = col >= a
+                const z ra = mk(rdl(pr[c].x, c2), -rdl(pr[c].y, c2));
+                if (lv && col >= a) pr[c2] = zsub(pr[c2], zmul(ra, pr[c]));
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int row = b0 + c;
+        if (lv && row < be && col >= row) Gs[row][col] = pr[c];
+      }
+      if (lane == 0) sbad = pbad;
+    }
     __syncthreads();
-    if (tid == 0) Gs[i][i] = mk(rii, 0);
-    for (int a = i + 1 + wv; a < n; a += NT / 64) {
-      const z ra = zcj(Gs[i][a]);
-      for (int b = a + lane; b < n; b += 64) Gs[a][b] = zsub(Gs[a][b], zmul(ra, Gs[i][b]));
+    if (sbad) { ok = false; break; }  // uniform
+    const int m = n - be;
+    for (int e = tid; e < m * m; e += NT) {
+      const int aa = e / m, bb = e - aa * m;
+      if (bb < aa) continue;
+      const int a = be + aa, b = be + bb;
+      z acc = Gs[a][b];
+      for (int i = b0; i < be; ++i) acc = zsub(acc, zmul(zcj(Gs[i][a]), Gs[i][b]));
+      Gs[a][b] = acc;
     }
     __syncthreads();
   }
+  // column j of R^-1 by the four lanes 4j .. 4j+3 (one wave holds 16 columns):
+  // each row's dot product split over the lanes, summed by two xor shuffles
+  // inside the group (its lanes run the same trip count), the entry written by
+  // the group's first lane and read back by all four (same wave: LDS in order)
   double inv2 = 0;
-  if (ok && tid < n) {
-    const int j = tid;
-    Rs[j][j] = mk(1.0 / Gs[j][j].x, 0);
-    inv2 = Rs[j][j].x * Rs[j][j].x;
-    for (int i = j - 1; i >= 0; --i) {
-      z acc = mk(0, 0);
-      for (int l = i + 1; l <= j; ++l) acc = zadd(acc, zmul(Gs[i][l], Rs[l][j]));
-      const z v = zsc(acc, -1.0 / Gs[i][i].x);
-      Rs[i][j] = v;
-      inv2 += v.x * v.x + v.y * v.y;
+  {
+    const int j = tid >> 2, s4 = tid & 3;
+    if (ok && j < n) {
+      const double djj = 1.0 / Gs[j][j].x;
+      if (s4 == 0) {
+        Rs[j][j] = mk(djj, 0);
+        inv2 = djj * djj;
+      }
+      for (int i = j - 1; i >= 0; --i) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        z acc = mk(0, 0);
+        for (int l = i + 1 + s4; l <= j; l += 4) acc = zadd(acc, zmul(Gs[i][l], Rs[l][j]));
+        acc.x += __shfl_xor(acc.x, 1, 64);
+        acc.y += __shfl_xor(acc.y, 1, 64);
+        acc.x += __shfl_xor(acc.x, 2, 64);
+        acc.y += __shfl_xor(acc.y, 2, 64);
+        const z v = zsc(acc, -1.0 / Gs[i][i].x);
+        if (s4 == 0) {
+          Rs[i][j] = v;
+          inv2 += v.x * v.x + v.y * v.y;
+        }
+      }
     }
   }
   inv2 = block_sum(inv2, red);  // uniform ok: every thread takes the same path
@@ -795,13 +864,6 @@ __device__ __forceinline__ T block_sum_r(T v, T* red) {
   return s;
 }
 
-// lane l's value of v (l uniform)
-__device__ __forceinline__ double rdl(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(unsigned long long)b, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
 
 // Blocked right-looking Cholesky G = L L^T of the lower triangle of G
 // (order k <= 128, ld ldg, LDS) by the workgroup, 16 columns per block: wave 0
