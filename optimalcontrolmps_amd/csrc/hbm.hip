@@ -192,7 +192,7 @@ struct Engine {
   // OCG_GEMM_STATS=1: shape statistics of the GEMM launches, printed at destruction (diagnostic)
   bool gstat = std::getenv("OCG_GEMM_STATS") != nullptr;
   long eig_hist[34] = {0};  // Gram block orders in bins of 16 (OCG_GEMM_STATS)
-  double gs_pad = 0, gs_flop = 0, gs_tiles_hist[6] = {0}, gs_flop_m[6] = {0}, gs_flop_k[6] = {0};
+  double gs_pad = 0, gs_iss = 0, gs_flop = 0, gs_tiles_hist[6] = {0}, gs_flop_m[6] = {0}, gs_flop_k[6] = {0};
   long gs_launch_hist[6] = {0};
   double gs_ms[6] = {0}, gs_bflop[6] = {0}, gs_ntask[6] = {0}, gs_nseg[6] = {0}, gs_m[6] = {0}, gs_n[6] = {0}, gs_k[6] = {0};
   std::vector<int> gs_evb;  // bucket of each pending gemm_ev pair
@@ -238,7 +238,8 @@ struct Engine {
     if (gstat && gemm_launches) {
       if (st) (void)hipStreamSynchronize(st);
       resolve_timers();
-      std::fprintf(stderr, "[gemm] launches %ld  alg/padded flops %.3f\n", gemm_launches, gs_flop / std::max(gs_pad, 1.0));
+      std::fprintf(stderr, "[gemm] launches %ld  alg/padded flops %.3f  alg/issued (live 16x16 units) %.3f\n", gemm_launches,
+                   gs_flop / std::max(gs_pad, 1.0), gs_flop / std::max(gs_iss, 1.0));
       const char* lb[6] = {"<32", "<64", "<128", "<256", "<512", ">=512"};
       for (int b = 0; b < 6; ++b)
         std::fprintf(stderr, "[gemm] %-6s launches(tiles/8) %ld  tiles %.0f  ms %.1f  TF %.2f  flop share by max(m,n) %.3f  by k %.3f\n", lb[b],
@@ -597,6 +598,7 @@ struct Engine {
           const double f = 8.0 * x.m * x.n * g.k;
           gs_flop += f;
           gs_pad += 8.0 * ((x.m + 31) / 32 * 32) * ((x.n + 31) / 32 * 32) * ((g.k + 3) / 4 * 4);
+          gs_iss += 8.0 * ((x.m + 15) / 16 * 16) * ((x.n + 15) / 16 * 16) * ((g.k + 3) / 4 * 4);
           gs_flop_m[gs_bucket(std::max(x.m, x.n))] += f;
           gs_flop_k[gs_bucket(g.k)] += f;
         }

@@ -136,6 +136,10 @@ __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, co
   const int ntn = (T.n + GT - 1) / GT;
   const int m0 = (tl / ntn) * GT, n0 = (tl % ntn) * GT;
   const int wm = (wv >> 1) * 16, wn = (wv & 1) * 16;
+  // a wave whose 16x16 sub-tile lies wholly outside the task (m or n not a
+  // multiple of 32: 25 % of the config-4 MFMA work) still stages operands but
+  // issues no MFMA; its outputs are never stored, so nothing else changes
+  const bool live = m0 + wm < T.m && n0 + wn < T.n;
   d4 cr = {0, 0, 0, 0}, ci = {0, 0, 0, 0};
   for (int s = 0; s < T.nseg; ++s) {
     const GSeg S = segs[T.seg0 + s];
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, co
       if (k0 + GK < S.k) gload(k0 + GK);
 #pragma unroll
       for (int ks = 0; ks < GK; ks += 4) {
-        if (k0 + ks < S.k) {  // k-steps past the end would only add zeros
+        if (live && k0 + ks < S.k) {  // k-steps past the end would only add zeros
           const int ar = wm + (lane & 15), kk = ks + (lane >> 4), bc = wn + (lane & 15);
           const double are = Ar[ar][kk], aim = Ai[ar][kk];
           const double bre = Br[kk][bc], bim = Bi[kk][bc];
