@@ -623,13 +623,14 @@ struct Engine {
       }
       gs_tiles_hist[b] += tiles;
     }
-    std::vector<int> tmap(static_cast<size_t>(tiles));
+    // per tile: its task and the task's first segment (-1: none)
+    std::vector<int2> tmap(static_cast<size_t>(tiles));
     for (size_t i = 0; i < t.size(); ++i) {
       const int e = i + 1 < t.size() ? t[i + 1].tile0 : tiles;
-      std::fill(tmap.begin() + t[i].tile0, tmap.begin() + e, int(i));
+      std::fill(tmap.begin() + t[i].tile0, tmap.begin() + e, make_int2(int(i), t[i].nseg > 0 ? t[i].seg0 : -1));
     }
     const GTask* dt_;
-    const int* dmap;
+    const int2* dmap;
     const GSeg* ds;
     upload3(t, tmap, segs, dt_, dmap, ds);
     hipEvent_t a = get_event(), b = get_event();

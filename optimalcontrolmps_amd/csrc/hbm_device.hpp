@@ -119,7 +119,7 @@ constexpr int GT = 32, GK = 16;
 // MI355X_MICROARCH.md §Workgroup dispatch) take consecutive tiles, so a task's
 // tiles share that XCD's L2 for their common operand rows / columns (speed
 // only: any bijection of workgroups onto tiles computes the same result)
-__global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, const int* __restrict__ tile_task,
+__global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, const int2* __restrict__ tile_task,
                                              const GSeg* __restrict__ segs, int xcd) {
   constexpr int EA = GT * GK / NT;  // staged elements per thread and operand
   __shared__ double Ar[GT][GK + 1], Ai[GT][GK + 1], Br[GK][GT + 1], Bi[GK][GT + 1];
@@ -129,9 +129,13 @@ __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, co
     const int nb = gridDim.x, base = nb >> 3, rem = nb & 7, x = blockIdx.x & 7;
     tile = x * base + (x < rem ? x : rem) + (blockIdx.x >> 3);
   }
-  // tile -> task from the host's table: one dependent load instead of a binary
-  // search over freshly uploaded task records (the small launches' latency)
-  const GTask T = tasks[tile_task[tile]];
+  // tile -> (task, its first segment) from the host's table: one dependent load
+  // instead of a binary search over freshly uploaded task records, then the
+  // task and first-segment records in parallel (the small launches' latency)
+  const int2 tt = tile_task[tile];
+  const GTask T = tasks[tt.x];
+  GSeg S0{};
+  if (tt.y >= 0) S0 = segs[tt.y];
   const int tl = tile - T.tile0;
   const int ntn = (T.n + GT - 1) / GT;
   const int m0 = (tl / ntn) * GT, n0 = (tl % ntn) * GT;
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, co
   const bool live = m0 + wm < T.m && n0 + wn < T.n;
   d4 cr = {0, 0, 0, 0}, ci = {0, 0, 0, 0};
   for (int s = 0; s < T.nseg; ++s) {
-    const GSeg S = segs[T.seg0 + s];
+    const GSeg S = s == 0 ? S0 : segs[T.seg0 + s];
     const bool ca = S.ops & 1, cb = (S.ops >> 1) & 1;
     // global -> registers for the chunk at k0 (issued one chunk ahead of its MFMAs)
     z va[EA], vb[EA];
