@@ -76,10 +76,14 @@ def main(tag, outdir=None):
     extra = {}
     mdb = db("pmc_mfma", tag)
     if os.path.exists(mdb):
-        for cn in ("SQ_INSTS_VALU_MFMA_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
-                   "SQ_INSTS_VALU_FMA_F64", "GRBM_GUI_ACTIVE"):
-            for k, (v, n) in pmc(mdb, cn).items():
-                extra.setdefault(k, {})[cn + "_per_dispatch"] = v / n
+        try:
+            for cn in ("SQ_INSTS_VALU_MFMA_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES",
+                       "SQ_INSTS_VALU_FMA_F64", "GRBM_GUI_ACTIVE"):
+                for k, (v, n) in pmc(mdb, cn).items():
+                    extra.setdefault(k, {})[cn + "_per_dispatch"] = v / n
+        except sqlite3.Error as e:  # a pass killed at its time limit leaves a partial database
+            print(f"  MFMA pass database unreadable ({e}); pmc_issue left empty", flush=True)
+            extra = {}
     summary = dict(tag=tag, kernels=ks, pmc_per_dispatch=per, pmc_issue=extra,
                    note="rocprofv3 --kernel-trace --stats and separate --pmc passes (FETCH_SIZE, WRITE_SIZE, "
                         "MFMA/issue counters) of the same `python3 bench.py` command; FETCH_SIZE doubled per the "
