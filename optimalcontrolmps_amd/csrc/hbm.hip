@@ -495,6 +495,12 @@ struct Engine {
     }
   };
   Arena work, tdev, thost;
+  // error paths: wait for everything queued on this engine's streams (the side
+  // stream's eigenvalue kernels read task lists and workspace the next call reuses)
+  void drain() {
+    (void)hipStreamSynchronize(st);
+    if (st2) (void)hipStreamSynchronize(st2);
+  }
   void sync() {
     HCK(hipStreamSynchronize(st));
     resolve_timers();
@@ -2174,8 +2180,13 @@ int guard(hbm_engine* h, F f) {
     h->err = e.what();
     rc = 3;
   }
-  (void)hipStreamSynchronize(h->E->st);
+  h->E->drain();
   h->E->release_all();
+  for (auto& W : h->W)
+    if (W) {
+      W->drain();
+      W->release_all();
+    }
   return rc;
 }
 struct Timer {
@@ -2441,6 +2452,21 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
     const int extra0 = h->xih_base() + N + 2;
     auto pb = [&](int k) { return k == 0 ? h->psi_base() : extra0 + 2 * N * (k - 1); };
     auto xb = [&](int k) { return k == 0 ? h->xi_base() : extra0 + 2 * N * (k - 1) + N; };
+    // the other controls' trajectories are not kept: their slots are given back
+    // afterwards, on success and on failure, down to the heap the call began with
+    // (a previous pipelined getHessian's row-state slots stay for its next call)
+    const size_t keep = std::max(size_t(extra0), E.heap_slots);
+    struct Shrink {
+      hbm::Engine& E;
+      size_t keep;
+      ~Shrink() {
+        try {
+          E.drain();
+          E.shrink_states(keep);
+        } catch (...) {
+        }
+      }
+    } shrink{E, keep};
     E.reserve_states(size_t(extra0) + size_t(2) * N * (K - 1));
     E.reserve_chains(std::max(E.nchain_cap, 2 * K), false);
     std::vector<Chain*> cs(2 * K);
@@ -2484,9 +2510,6 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
     for (int k = 0; k < K; ++k) fx[k] = pb(k) + N - 1;
     auto rf = hbm_pairs(h, fx, fy, false);
     for (int k = 0; k < K; ++k) { F[2 * k] = rf[k].real(); F[2 * k + 1] = rf[k].imag(); }
-    // the other controls' trajectories are not kept: give their slots back so the
-    // free-memory checks of later calls (checkpointing, row batches) see them
-    E.shrink_states(size_t(extra0));
   });
 }
 
@@ -2613,6 +2636,15 @@ static double heap_growth_bytes(const hbm_engine* h, double slots) {
   return slots <= double(h->E->heap_slots) ? 0.0 : 16.0 * double(h->E->state_cap) * slots;
 }
 double hbm_traj_bytes(const hbm_engine* h, int N) { return heap_growth_bytes(h, 3.0 * N + 6.0); }
+// bytes a pool of n chains (with their share of the workspace, as hbm_batch
+// prices them) would newly allocate on an engine holding `have` chains
+static double chain_growth_bytes(const hbm::Engine& E, int n, int have, bool wide) {
+  return n <= have ? 0.0 : 16.0 * 4.0 * double(E.chain_elems(wide)) * n;
+}
+double hbm_gradient_multi_bytes(const hbm_engine* h, int K, int N) {
+  const hbm::Engine& E = *h->E;
+  return heap_growth_bytes(h, 3.0 * N + 6.0 + 2.0 * N * (K - 1)) + chain_growth_bytes(E, 2 * K, E.nchain_cap, false);
+}
 
 // Checkpointed getHessian (see hbm.hpp).  Time-major row sweep: all rows of a
 // batch advance together in absolute time j (row i joins at j = i with
@@ -2943,7 +2975,16 @@ int pipe_psih_base(const hbm_engine* h, int N) { return 4 + 3 * N + 2; }
 double hbm_pipe_bytes(const hbm_engine* h, int N, const int* rows, int nrows) {
   double slots = pipe_psih_base(h, N) + N;
   for (int r = 0; r < nrows; ++r) slots += std::max(0, N - 2 - rows[r]);
-  return heap_growth_bytes(h, slots);
+  const hbm::Engine& E = *h->E;
+  // + the context engine's nrows + 1 chains (psi and every joined row) and the two
+  // workers' pools: the dH worker joins up to 8 rows (normal + wide chains), the
+  // xi worker applies dH in chunks of up to min(N, 8) states
+  const int wn[2] = {h->W[0] ? h->W[0]->nchain_cap : 0, h->W[1] ? h->W[1]->nchain_cap : 0};
+  const int ww[2] = {h->W[0] ? h->W[0]->nchain_cap_w : 0, h->W[1] ? h->W[1]->nchain_cap_w : 0};
+  const int xc = std::min(N, 8);
+  return heap_growth_bytes(h, slots) + chain_growth_bytes(E, nrows + 1, E.nchain_cap, false) +
+         chain_growth_bytes(E, 8, wn[0], false) + chain_growth_bytes(E, 8, ww[0], true) +
+         chain_growth_bytes(E, xc, wn[1], false) + chain_growth_bytes(E, xc, ww[1], true);
 }
 
 int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
@@ -2959,6 +3000,21 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
     std::vector<int> rsoff(nrows + 1);
     rsoff[0] = psih0 + N;
     for (int k = 0; k < nrows; ++k) rsoff[k + 1] = rsoff[k] + (N - 2 - rs[k]);
+    // a failed call gives its row-state slots back (the caller then runs the
+    // two-phase path, which must see that memory free)
+    struct ShrinkOnError {
+      hbm::Engine& E;
+      size_t keep;
+      bool ok = false;
+      ~ShrinkOnError() {
+        if (ok) return;
+        try {
+          E.drain();
+          E.shrink_states(keep);
+        } catch (...) {
+        }
+      }
+    } undo{E, std::max(E.heap_slots, size_t(h->xih_base() + N + 2))};
     E.reserve_states(size_t(rsoff[nrows]));
     hbm::Engine& WH = pipe_worker(h, 0);
     hbm::Engine& WX = pipe_worker(h, 1);
@@ -3185,5 +3241,6 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
       }
     }
     tall.stop(long(N - 1) * 2 + long(rsoff[nrows] - rsoff[0]));
+    undo.ok = true;
   });
 }

@@ -52,6 +52,9 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
 // bytes the stored-trajectory Hessian's 3 N + 6 state slots would newly allocate
 // (0 when the context's state heap already holds them)
 double hbm_traj_bytes(const hbm_engine* h, int N);
+// bytes hbm_gradient_multi would newly allocate: its 3 N + 6 + 2 N (K - 1) state
+// slots and 2 K chains (0 when the engine already holds them)
+double hbm_gradient_multi_bytes(const hbm_engine* h, int K, int N);
 int hbm_get_state(hbm_engine* h, int which, int t, int* dims, double* data, size_t cap, size_t* nelem);
 // kinds 0-6 as ocg_kernel_stats (HIP-event phase times); 7: the MFMA GEMM
 // kernel (k_gemm) with its algorithmic bytes and flops
@@ -73,6 +76,7 @@ int hbm_ground_state(hbm_engine* h, const int* dims, const double* data, double 
 // for one batched overlap pass; bit-identical to propagate + xi_dH + rows
 int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int nrows, double* H, double* divT,
                      double* F);
-// heap bytes hbm_hessian_pipe would newly allocate for its slots (trajectories +
-// psiH_i + row states; 0 when the heap already holds them, e.g. from the last call)
+// bytes hbm_hessian_pipe would newly allocate: its slots (trajectories + psiH_i +
+// row states; 0 when the heap already holds them, e.g. from the last call) and the
+// chain pools of the context engine (psi + every row) and of the two workers
 double hbm_pipe_bytes(const hbm_engine* h, int N, const int* rows, int nrows);

@@ -1012,18 +1012,16 @@ int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, 
   if (!c || !u || !divT || !F || N < 2 || K < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
   if (size_t(K) * 4 * size_t(N) + 6 > size_t(INT32_MAX)) return fail(c, OCG_EINVAL, "K * N too large");
   if (c->hbm && K > 1) {
-    // One batch of 2K chains when the grown state heap fits half the free HBM,
+    // One batch of 2K chains when what it newly allocates fits half the free HBM,
     // else in turn.  The heap grows by copying into a new allocation while the
     // old one is live, so the whole new heap (the context's own 3N + 6 slots +
-    // 2N per extra control) must fit in the free memory; the extra slots are
-    // given back after the call (hbm_gradient_multi).  A batched call that
-    // still fails (allocation) falls back to the in-turn loop.
+    // 2N per extra control) counts, plus the 2K chains; the extra slots are
+    // given back after the call, also when it fails (hbm_gradient_multi).  A
+    // batched call that still fails (allocation) falls back to the in-turn loop.
     size_t fr = 0, tot = 0;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemGetInfo(&fr, &tot));
-    const double base = hbm_traj_bytes(c->hbm, N);
-    const double per_control = base * (2.0 * N) / (3.0 * N + 6.0);
-    if (base + per_control * (K - 1) <= 0.5 * double(fr)) {
+    if (hbm_gradient_multi_bytes(c->hbm, K, N) <= 0.5 * double(fr)) {
       c->u_psi.clear();
       c->u_xi.clear();
       if (hb(c, hbm_gradient_multi(c->hbm, K, u, N, divT, F)) == 0) {
@@ -1267,9 +1265,13 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
       if (hbm_pipe_bytes(c->hbm, N, rows, nrows) <= 0.5 * double(fr)) {
         c->u_psi.clear();
         c->u_xi.clear();
-        const int rc = hb(c, hbm_hessian_pipe(c->hbm, u, N, rows, nrows, H, divT, F));
-        if (!rc) note_u(c, u, N, 3);
-        return rc;
+        if (hb(c, hbm_hessian_pipe(c->hbm, u, N, rows, nrows, H, divT, F)) == 0) {
+          note_u(c, u, N, 3);
+          return 0;
+        }
+        // a pipeline that still fails (allocation of a worker's pools or arenas)
+        // has given its row-state slots back: the two-phase path runs instead and
+        // writes the same entries of H
       }
     }
     return hessian_unfused(c, u, N, rows, nrows, H, divT, F);

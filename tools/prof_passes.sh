@@ -4,7 +4,7 @@
 # (MI355X_MICROARCH.md HBM/rocprofv3 recipe), all over the same bench command.
 # The rocpd databases go to /tmp (gpurun_out/ must stay under 64 MiB); only the
 # summaries and logs land in gpurun_out/profiles_<tag>.
-# Usage: tools/profile_r02.sh <tag> [bench args...]   (PROF_TMO / PMC_TMO: per-pass time limits;
+# Usage: tools/prof_passes.sh <tag> [bench args...]   (PROF_TMO / PMC_TMO: per-pass time limits;
 # PROF_MFMA=0: no MFMA / issue-counter pass; it is the slowest pass of large runs (its database
 # generation), so a pass that runs out of time leaves the other passes' summaries intact)
 TAG=${1:-r02}

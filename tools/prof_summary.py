@@ -42,7 +42,7 @@ def pmc(db, counter):
 
 
 def db(kind, tag):
-    """rocpd database of one pass: $PROF_DB_ROOT/<kind>/ (tools/profile_r02.sh) or
+    """rocpd database of one pass: $PROF_DB_ROOT/<kind>/ (tools/prof_passes.sh) or
     gpurun_out/<kind>_<tag>/ (older layout)"""
     root = os.environ.get("PROF_DB_ROOT")
     if root:
