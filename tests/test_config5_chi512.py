@@ -1,0 +1,147 @@
+"""BASELINE configs[4] at its real bond dimension: L=50, Npart=50, d=8 (p=9),
+tstep=0.01, cutoff 1e-8, Maxm 512, from a state saturated at chi = 512 on the
+device (the Mott state |1..1> evolved 230 steps at U=2.5, as bench.py
+--workload c5rows prepares it; ~30 s).  Every decomposition of these steps
+runs the blocked large-order eigensolver (Gram orders 209..512), the MFMA
+GEMMs at m, n, k ~ 500 and the certified gauge moves at those orders.
+
+The CPU oracle cannot step this chain in test time (its cyclic Jacobi needs
+hours per chi = 512 step), so parity here is the reference's own property
+tests at the reference's tolerances plus path equalities:
+* the analytic gradient vs central differences of the cost
+  (tests/GradientTests.cpp:140-143: 0.1 %),
+* the interior fidelity Hessian vs central differences of the analytic
+  gradient (tests/HessianTests.cpp:178-205: 0.5 %),
+* batched steps == single steps, pipelined getHessian == stored two-phase
+  getHessian, bit for bit,
+* certified CholeskyQR2 gauge moves vs the eigen path: same bond dimensions,
+  states overlapping to 1 - 1e-11.
+N_t = 4 (2 interior controls, 3 steps per trajectory)."""
+import numpy as np
+import pytest
+
+L, p, N, J, DT, CUT, MAXM = 50, 9, 50, 1.0, 0.01, 1e-8, 512
+NT = 4
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
+
+
+@pytest.fixture(scope="module")
+def warm512():
+    from optimalcontrolmps_amd.native import Engine
+    from optimalcontrolmps_amd.states import product_state, warm_state
+    eng = Engine(L, p, N, J, DT, CUT, MAXM, engine="hbm")
+    ini = warm_state(eng, product_state(L, p, N), 2.5, 230, chunk=10)
+    tgt = eng.steps(ini, np.full(3, 6.0), True)   # overlapping target (bench.py c4/c5 workloads)
+    eng.close()
+    return ini, tgt
+
+
+def _engine(monkeypatch=None, **env):
+    from optimalcontrolmps_amd.native import Engine
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    return Engine(L, p, N, J, DT, CUT, MAXM, engine="hbm")
+
+
+def test_c5_w512_saturated(warm512):
+    ini, tgt = warm512
+    b = ini.bond_dims()
+    assert b.max() == MAXM
+    assert (b[5:-5] == MAXM).mean() > 0.8     # saturated across the bulk of the chain
+    eng = _engine()
+    assert abs(eng.overlap(ini, ini) - 1.0) <= 1e-12
+    assert abs(eng.overlap(tgt, tgt) - 1.0) <= 1e-12
+    assert 1e-3 < abs(eng.overlap(tgt, ini)) < 1.0
+    eng.close()
+
+
+def _gradient(eng, u):
+    eng.propagate(u, 3)
+    return DT * (eng.div_t() * eng.overlap_factor() * 1j).real
+
+
+def test_c5_w512_gradient_fd(warm512):
+    ini, tgt = warm512
+    eng = _engine()
+    eng.set_states(tgt, ini)
+    u = np.random.default_rng(50).uniform(2.0, 10.0, NT)
+
+    def cost(v):
+        eng.propagate(v, 1)
+        return 0.5 * (1.0 - abs(eng.overlap_factor()) ** 2)
+
+    g = _gradient(eng, u)
+    eps = 1e-4
+    for i in range(1, NT - 1):
+        up, um = u.copy(), u.copy()
+        up[i] += eps
+        um[i] -= eps
+        num = (cost(up) - cost(um)) / (2 * eps)
+        assert abs(g[i] - num) <= 1e-3 * abs(num) + 1e-12, (i, g[i], num)
+    eng.close()
+
+
+def test_c5_w512_hessian_fd(warm512):
+    ini, tgt = warm512
+    eng = _engine()
+    eng.set_states(tgt, ini)
+    u = np.random.default_rng(51).uniform(2.0, 10.0, NT)
+    H, divT, F = eng.hessian(u)
+    assert np.array_equal(H, H.T)
+    g0 = DT * (divT * F * 1j).real
+    assert np.abs(g0 - _gradient(eng, u)).max() <= 1e-12 * np.abs(g0).max()
+    eps = 1e-3
+    for j in range(1, NT - 1):
+        up, um = u.copy(), u.copy()
+        up[j] += eps
+        um[j] -= eps
+        col = (_gradient(eng, up) - _gradient(eng, um)) / (2 * eps)
+        for i in range(1, NT - 1):
+            assert abs(H[i, j] - col[i]) <= 5e-3 * abs(col[i]) + 1e-12, (i, j, H[i, j], col[i])
+    eng.close()
+
+
+def test_c5_w512_batched_equals_single(warm512):
+    ini, tgt = warm512
+    eng = _engine()
+    uf, ut = np.array([2.5, 9.0, 4.0]), np.array([3.0, 7.5, 2.0])
+    states = [ini, tgt, ini]
+    batched = eng.step_batch(states, uf, ut, True)
+    for i, s in enumerate(states):
+        single = eng.step(s, uf[i], ut[i], True)
+        assert np.array_equal(single.dims, batched[i].dims)
+        assert np.array_equal(single.data, batched[i].data)
+    back = eng.step_batch([ini, tgt], uf[:2], ut[:2], False)
+    for i, s in enumerate([ini, tgt]):
+        single = eng.step(s, uf[i], ut[i], False)
+        assert np.array_equal(single.dims, back[i].dims)
+        assert np.array_equal(single.data, back[i].data)
+    eng.close()
+
+
+def test_c5_w512_pipelined_equals_stored(warm512, monkeypatch):
+    ini, tgt = warm512
+    u = np.random.default_rng(52).uniform(2.0, 10.0, NT)
+    out = {}
+    for mode in ("0", "1"):
+        eng = _engine(monkeypatch, OCG_HBM_PIPE=mode)
+        eng.set_states(tgt, ini)
+        out[mode] = eng.hessian(u)
+        eng.close()
+    (H0, d0, F0), (H1, d1, F1) = out["0"], out["1"]
+    assert np.array_equal(H0, H1) and np.array_equal(d0, d1) and F0 == F1
+
+
+def test_c5_w512_certified_vs_eigen_gauge(warm512, monkeypatch):
+    ini, _ = warm512
+    res = {}
+    for fast in ("1", "0"):
+        eng = _engine(monkeypatch, OCG_HBM_FASTGAUGE=fast)
+        res[fast] = (eng, eng.steps(ini, np.array([2.5, 3.0, 3.5]), True))
+    (e1, s1), (e0, s0) = res["1"], res["0"]
+    assert list(s1.bond_dims()) == list(s0.bond_dims())
+    assert abs(e1.overlap(s1, s0) - 1.0) <= 1e-11
+    assert abs(e1.overlap(s1, s1) - 1.0) <= 1e-12
+    e1.close()
+    e0.close()

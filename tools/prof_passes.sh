@@ -21,6 +21,11 @@ L=$R/gpurun_out/profiles_$TAG
 ( while true; do date >> $L/heartbeat.txt; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
+# PREP_ARGS: an unprofiled bench run first (e.g. --prepare-only --state-cache ...: the
+# c4/c5 warm states), so the profiled command holds only the timed population
+if [ -n "$PREP_ARGS" ]; then
+  timeout -k 10 ${PREP_TMO:-300} python3 $R/bench.py $PREP_ARGS > $L/prep_$TAG.log 2>&1 || exit $?
+fi
 timeout -k 10 $T1 rocprofv3 --kernel-trace --stats -d $D/prof -o run -- python3 $R/bench.py $ARGS > $L/prof_$TAG.log 2>&1 || exit $?
 timeout -s KILL $T2 rocprofv3 --pmc FETCH_SIZE -d $D/pmc_fetch -o run -- python3 $R/bench.py $ARGS > $L/pmc_fetch_$TAG.log 2>&1 || exit $?
 timeout -s KILL $T2 rocprofv3 --pmc WRITE_SIZE -d $D/pmc_write -o run -- python3 $R/bench.py $ARGS > $L/pmc_write_$TAG.log 2>&1 || exit $?
