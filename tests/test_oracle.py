@@ -5,6 +5,8 @@ independent exact state-vector implementation of the same Trotter scheme
 (Hermitian eigensolver, ITensor truncation rule).  The reference's own golden
 numbers are checked through the facade in test_facade_cpu.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -116,3 +118,33 @@ def test_truncation_rule():
     assert O.truncate(P, 0.06, 2) == 2
     assert O.truncate(P, 0.99, 100) == 1
     assert O.truncate(np.array([1.0]), 0.5, 100) == 1
+
+
+def test_hessian_formula_first_order_in_dt():
+    """calcHessianRow (src/OptimalControl.cpp:251-279) takes d psi_j / d u_i to
+    first order in dt, so the analytic Hessian differs from the derivative of
+    the analytic gradient by O(dt): measured on the oracle at config 4's chain
+    (L=20, p=7, Maxm 32, psi_target near psi_init, N_t = 4), the gap halves
+    with dt.  The chi = 512 GPU test (tests/test_config5_chi512.py) relies on
+    this scaling instead of HessianTests' 5e-3, which holds only at the
+    reference's own L = 5 test shape."""
+    import oracle_ffi as O
+    z = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "c4.npz"), allow_pickle=False))
+    L, p, N, J, CUT = 20, 7, 20, 1.0, 1e-8
+    tgt = O.MPS(L, p, N, z["s32/tgt_dims"], z["s32/tgt_data"])
+    ini = O.MPS(L, p, N, z["s32/init_dims"], z["s32/init_data"])
+    u = np.random.default_rng(51).uniform(2.0, 10.0, 4)
+    gaps = []
+    for dt in (0.01, 0.005):
+        oc = O.OC(O.Stepper(L, p, N, J, dt, CUT, int(z["s32/maxm"])), tgt, ini, 4, 0.0)
+        H = oc.hessian(u, 4)
+        eps, gap = 1e-3, 0.0
+        for j in (1, 2):
+            up, um = u.copy(), u.copy()
+            up[j] += eps
+            um[j] -= eps
+            col = (oc.gradient(up) - oc.gradient(um)) / (2 * eps)
+            gap = max(gap, float(np.max(np.abs(H[1:3, j] - col[1:3]) / np.abs(col[1:3]))))
+        gaps.append(gap)
+    assert 0.02 < gaps[0] < 0.05           # 3.7 % at dt = 0.01
+    assert 0.25 < gaps[1] / gaps[0] < 0.6  # 1.4 % at dt = 0.005
