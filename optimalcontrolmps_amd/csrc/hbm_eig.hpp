@@ -327,13 +327,15 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
     if (tid == 0) {
       P.tau[j] = tau;
       sbeta[j] = beta;
-      u[j + 1] = u0;  // nobody reads u[j + 1] before barrier A'
     }
     STAMP(2);
-    lds_barrier();  // A': u complete
-    STAMP(3);
+    // every thread computed the same u0: element j + 1 of the Householder vector
+    // is taken from the register (the LDS copy still holds alpha until
+    // colprep(j + 2) clears it), so no barrier publishes it
+    const int j1 = j + 1;
+    auto uat = [&](int i) { return i == j1 ? u0 : u[i]; };
     // Householder vector -> column j of P.A (rows j+1 ..)
-    for (int i = j + 1 + tid; i < n; i += RNT) P.A[(size_t)i * n + j] = u[i];
+    for (int i = j + 1 + tid; i < n; i += RNT) P.A[(size_t)i * n + j] = uat(i);
     const int a0 = (j + 1) >> 4;  // first live slot row / column (uniform)
     if (tau != 0.0) {  // uniform: every thread computed the same reflector
       // ---- p = tau A_t u (lower storage: row and column contributions)
@@ -341,13 +343,13 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
       z uk[RAT], cp[RAT];
 #pragma unroll
       for (int b = 0; b < RAT; ++b) {
-        uk[b] = (b >= a0 && b < aend) ? u[16 * b + c] : mk(0, 0);
+        uk[b] = (b >= a0 && b < aend) ? uat(16 * b + c) : mk(0, 0);
         cp[b] = mk(0, 0);
       }
 #pragma unroll
       for (int a = 0; a < RAT; ++a) {
         if (a < a0 || a >= aend) continue;
-        const z ui = u[16 * a + r];
+        const z ui = uat(16 * a + r);
         z acc = mk(0, 0);
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
@@ -384,7 +386,7 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
           for (int q = 0; q < 16; ++q) sacc = zadd(sacc, zadd(rowbuf[a][cc][q], colbuf[a][q][cc]));
           const z pk = zsc(sacc, tau);
           sp[k] = pk;
-          const z ukk = u[k];
+          const z ukk = uat(k);
           kp = ukk.x * pk.x + ukk.y * pk.y;
         }
         if (tid == 0) sp[j] = mk(0, 0);  // leaves the trailing block
@@ -408,7 +410,7 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
       for (int a = 0; a < RAT; ++a) {
         if (a < a0 || a >= aend) continue;
         const int i = 16 * a + r;
-        const z ui = u[i];
+        const z ui = uat(i);
         const z wi = zsub(sp[i], zsc(ui, K));
 #pragma unroll
         for (int b = 0; b <= a; ++b) {

@@ -99,7 +99,33 @@ def make_w256h(out, Nt=5):
                 "w256h/grad": g, "w256h/divT": divT, "w256h/F": np.array([F])})
 
 
+def make_w256h9():
+    """c4_w256h9.npz: the w256h setting (same saturated psi_init and psi_target,
+    Maxm 256) at N_t = 9 GRAPE controls U(2,10) (seed 9256): divT, F, gradient
+    and the full fidelity Hessian (rows 1..7, up to 6 row steps each) on the
+    oracle with 8 threads (~3 h on this container); a file of its own (the
+    target comes from c4.npz's w256h/tgt_*)."""
+    z = np.load(os.path.join(HERE, "c4_warm256.npz"), allow_pickle=False)
+    c = load_out()
+    st = O.Stepper(L, p, N, J, DT, CUT, 256)
+    psi0 = O.MPS(L, p, N, z["dims"], z["data"])
+    tgt = O.MPS(L, p, N, c["w256h/tgt_dims"], c["w256h/tgt_data"])
+    Nt = 9
+    u = np.random.default_rng(9256).uniform(2.0, 10.0, Nt)
+    oc = O.OC(st, tgt, psi0, Nt, 0.0)
+    t0 = time.time()
+    H = oc.hessian(u, 8)
+    divT, F = oc.divT_F()
+    g = DT * (divT * F * 1j).real
+    print(f"w256h9 oracle hessian {time.time() - t0:.1f}s  max|H| {np.abs(H).max():.3e} "
+          f"max|g| {np.abs(g).max():.3e} F {F}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "c4_w256h9.npz"), u=u, H=H, grad=g, divT=divT, F=np.array([F]))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["w256h9"]:
+        make_w256h9()
+        sys.exit(0)
     which = sys.argv[1:] or ["s32", "w256"]
     out = load_out()
     if "s32" in which:

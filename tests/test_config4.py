@@ -301,3 +301,28 @@ def test_c4_w256_hessian_vs_oracle(c4, warm256, monkeypatch, pipe):
     assert np.abs(g - go).max() <= 1e-6
     assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
     eng.close()
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_c4_w256_hessian9_vs_oracle(c4, warm256, monkeypatch, pipe):
+    """config 4's real bond dimension at N_t = 9 (7 rows, up to 6 row steps: the
+    pipelined path's row joins over more rows than w256h's 3): gradient, divT,
+    F and the full fidelity Hessian against the oracle (tests/golden/
+    make_c4_fixtures.py w256h9, ~3 h on the CPU restatement) at the north_star
+    tolerances, through the pipelined and the stored getHessian"""
+    from optimalcontrolmps_amd.native import Engine
+    path = os.path.join(HERE, "golden", "c4_w256h9.npz")
+    if not os.path.exists(path):
+        pytest.skip("w256h9 oracle fixture not generated")
+    z = dict(np.load(path, allow_pickle=False))
+    monkeypatch.setenv("OCG_HBM_PIPE", pipe)
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    eng.set_states(_mps(c4["w256h/tgt_dims"], c4["w256h/tgt_data"]), warm256)
+    H, divT, F = eng.hessian(z["u"])
+    g = DT * (divT * F * 1j).real
+    Fo = complex(z["F"][0])
+    assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12
+    assert np.abs(divT - z["divT"]).max() <= 1e-8 * np.abs(z["divT"]).max()
+    assert np.abs(g - z["grad"]).max() <= 1e-6
+    assert np.abs(H - z["H"]).max() <= 1e-6 * np.abs(z["H"]).max()
+    eng.close()
