@@ -222,6 +222,8 @@ struct ocg_ctx {
   // fused pipeline (ocg_hessian)
   Pool rs{nullptr, nullptr};  // stored psiH_i(j) states
   size_t rs_cap = 0;
+  char* h_pin = nullptr;      // pinned host staging of the fused getHessian's uploads / results
+  size_t pin_cap = 0;
   int* d_flags = nullptr;     // [2N] psi / xi publication epochs
   int flags_cap = 0;
   int flags_N = -1, flags_K = -1;  // (N, K) layout of the flag buffer's current epoch run
@@ -321,6 +323,20 @@ static int ensure_buf(ocg_ctx* c, T*& ptr, int& cap, int n) {
   int m = std::max(n, 2 * cap);
   HIPCHK(c, hipMalloc(&ptr, sizeof(T) * size_t(m)));
   cap = m;
+  return 0;
+}
+
+// pinned host staging of at least `bytes` (the stream is drained before a
+// reallocation: queued copies may still use the old buffer)
+static int ensure_pin(ocg_ctx* c, size_t bytes) {
+  if (bytes <= c->pin_cap) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->h_pin) (void)hipHostFree(c->h_pin);
+  c->h_pin = nullptr;
+  c->pin_cap = 0;
+  const size_t m = std::max(bytes, 2 * c->pin_cap);
+  HIPCHK(c, hipHostMalloc((void**)&c->h_pin, m, hipHostMallocDefault));
+  c->pin_cap = m;
   return 0;
 }
 
@@ -667,6 +683,7 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->d_u) (void)hipFree(c->d_u);
   if (c->d_c) (void)hipFree(c->d_c);
   if (c->d_H) (void)hipFree(c->d_H);
+  if (c->h_pin) (void)hipHostFree(c->h_pin);
   if (c->d_norms) (void)hipFree(c->d_norms);
   if (c->d_rnorm) (void)hipFree(c->d_rnorm);
   if (c->d_idx2) (void)hipFree(c->d_idx2);
@@ -1363,8 +1380,19 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
     c->H_cap = hn;
   }
   const int epoch = ++c->epoch;
-  HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * K * N, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_rows, rb.data(), sizeof(int) * rb.size(), hipMemcpyHostToDevice, c->stream));
+  // pinned staging: [u | row table | pair lists] uploaded, [err | divT, F | H]
+  // downloaded, all as DMA copies (pageable copies are staged and block)
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t nidx = 2 * size_t(K) * N + 2 * K;
+  const size_t o_rb = al(sizeof(double) * K * N), o_idx = o_rb + al(sizeof(int) * rb.size());
+  const size_t o_err = o_idx + al(sizeof(int) * nidx), o_pc = o_err + 256;
+  const size_t o_h = o_pc + al(sizeof(zc) * K * (N + 1)), pin_bytes = o_h + sizeof(double) * hn;
+  if (int rc = ensure_pin(c, pin_bytes)) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // no copy of an earlier (failed) call still reads the staging
+  std::memcpy(c->h_pin, u, sizeof(double) * K * N);
+  std::memcpy(c->h_pin + o_rb, rb.data(), sizeof(int) * rb.size());
+  HIPCHK(c, hipMemcpyAsync(c->d_u, c->h_pin, sizeof(double) * K * N, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_rows, c->h_pin + o_rb, sizeof(int) * rb.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_H, 0, sizeof(double) * hn, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_flags + K * (2 * N + 2), 0, sizeof(int), c->stream));  // role tickets
@@ -1372,7 +1400,7 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   const int* d_rbase = c->d_rows + nrows;
   // divT_i = <xi_i|dH|psi_i> and F = <psi_{N-1}|target> pair lists
   // K N dH pairs (xs then ys), then K F pairs (xs then ys)
-  std::vector<int> idx(2 * K * N + 2 * K);
+  int* idx = (int*)(c->h_pin + o_idx);
   for (int k = 0; k < K; ++k) {
     for (int i = 0; i < N; ++i) {
       idx[k * N + i] = c->xi_base() + k * cs + i;
@@ -1381,8 +1409,8 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
     idx[2 * K * N + k] = c->psi_base() + k * cs + N - 1;
     idx[2 * K * N + K + k] = c->slot_target();
   }
-  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, int(idx.size()))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, c->stream));
+  if (int rc = ensure_buf(c, c->d_idx, c->idx_cap, int(nidx))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_idx, idx, sizeof(int) * nidx, hipMemcpyHostToDevice, c->stream));
   // the three launches back to back, one host synchronisation at the end;
   // the phase marks give the per-kernel times (ocg_kernel_stats kinds 5, 1, 6)
   HIPCHK(c, hipEventRecord(c->evh[0], c->stream));
@@ -1430,13 +1458,13 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
                        c->d_pc + K * N, N, c->d_H, c->d_stats + 6 * 3, K, cs);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->evh[3], c->stream));
-  std::vector<zc> pc(size_t(K) * (N + 1));
-  std::vector<double> h(hn);
-  int err = 0;
-  HIPCHK(c, hipMemcpyAsync(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(pc.data(), c->d_pc, sizeof(zc) * K * (N + 1), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost, c->stream));
+  const zc* pc = (const zc*)(c->h_pin + o_pc);
+  const double* h = (const double*)(c->h_pin + o_h);
+  HIPCHK(c, hipMemcpyAsync(c->h_pin + o_err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_pin + o_pc, c->d_pc, sizeof(zc) * K * (N + 1), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_pin + o_h, c->d_H, sizeof(double) * hn, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int err = *(const int*)(c->h_pin + o_err);
   const int kinds[3] = {5, 1, 6};
   for (int k = 0; k < 3; ++k) {
     if (k == 2 && total == 0) break;
@@ -1457,7 +1485,7 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   note_u(c, u, N, 3);  // control 0's trajectories stay in the context
   for (int k = 0; k < K; ++k) {
     double* Hk = H + size_t(k) * N * N;
-    const double* hk = h.data() + size_t(k) * N * N;
+    const double* hk = h + size_t(k) * N * N;
     for (int i = 0; i < N; ++i) {
       divT[2 * (size_t(k) * N + i)] = pc[size_t(k) * N + i].x;
       divT[2 * (size_t(k) * N + i) + 1] = pc[size_t(k) * N + i].y;
