@@ -93,6 +93,17 @@ int orc_heev(int n, const double* a /* 2 n^2 */, double* w, double* v /* 2 n^2 *
   for (size_t i = 0; i < V.size(); ++i) { v[2 * i] = V[i].real(); v[2 * i + 1] = V[i].imag(); }
   return 0;
 }
+// the Householder + QL solver (ORC_HEEV=ql) on its own, for its tests
+int orc_heev_ql(int n, const double* a /* 2 n^2 */, double* w, double* v /* 2 n^2 */) {
+  std::vector<cplx> A(size_t(n) * n);
+  for (size_t i = 0; i < A.size(); ++i) A[i] = cplx(a[2 * i], a[2 * i + 1]);
+  std::vector<double> ww;
+  std::vector<cplx> V;
+  heev_ql(n, A, ww, V);
+  for (int i = 0; i < n; ++i) w[i] = ww[i];
+  for (size_t i = 0; i < V.size(); ++i) { v[2 * i] = V[i].real(); v[2 * i + 1] = V[i].imag(); }
+  return 0;
+}
 
 int orc_truncate(const double* P, int n, double cutoff, int maxm) {
   return truncate_count(std::vector<double>(P, P + n), cutoff, maxm, 1);

@@ -14,7 +14,9 @@ c4.npz:
           <psi_1|dH|psi_1>.
   w256h/* Maxm = 256, N_t = 5: gradient and full fidelity Hessian from the
           saturated warm state (make_w256h).
-Run: python tests/golden/make_c4_fixtures.py [s32] [w256] [w256h]
+  c4_w256h<N>.npz: the w256h setting at N_t = N (make_w256hN, oracle with the
+          Householder + QL eigensolver).
+Run: python tests/golden/make_c4_fixtures.py [s32] [w256] [w256h]  |  w256h17
 """
 import os
 import sys
@@ -99,32 +101,37 @@ def make_w256h(out, Nt=5):
                 "w256h/grad": g, "w256h/divT": divT, "w256h/F": np.array([F])})
 
 
-def make_w256h9():
-    """c4_w256h9.npz: the w256h setting (same saturated psi_init and psi_target,
-    Maxm 256) at N_t = 9 GRAPE controls U(2,10) (seed 9256): divT, F, gradient
-    and the full fidelity Hessian (rows 1..7, up to 6 row steps each) on the
-    oracle with 8 threads (~3 h on this container); a file of its own (the
-    target comes from c4.npz's w256h/tgt_*)."""
+def make_w256hN(Nt):
+    """c4_w256h<Nt>.npz: the w256h setting (same saturated psi_init and
+    psi_target, Maxm 256) at a longer horizon, N_t GRAPE controls U(2,10)
+    (seed 9000 + N_t): divT, F, gradient and the full fidelity Hessian (rows
+    1..N_t-2, up to N_t-3 row steps each) on the oracle with 8 threads and the
+    Householder + QL block eigensolver (ORC_HEEV=ql: LAPACK zheev's algorithm;
+    the same bond dims and overlaps as the default cyclic Jacobi to ~5e-13 on
+    the w256 step, tests/test_oracle.py::test_heev_ql_vs_numpy_and_jacobi, and
+    ~14x faster: 27 s per chi = 256 step).  A file of its own; the target
+    comes from c4.npz's w256h/tgt_*."""
+    assert os.environ.get("ORC_HEEV") == "ql"
     z = np.load(os.path.join(HERE, "c4_warm256.npz"), allow_pickle=False)
     c = load_out()
     st = O.Stepper(L, p, N, J, DT, CUT, 256)
     psi0 = O.MPS(L, p, N, z["dims"], z["data"])
     tgt = O.MPS(L, p, N, c["w256h/tgt_dims"], c["w256h/tgt_data"])
-    Nt = 9
-    u = np.random.default_rng(9256).uniform(2.0, 10.0, Nt)
+    u = np.random.default_rng(9000 + Nt).uniform(2.0, 10.0, Nt)
     oc = O.OC(st, tgt, psi0, Nt, 0.0)
     t0 = time.time()
     H = oc.hessian(u, 8)
     divT, F = oc.divT_F()
     g = DT * (divT * F * 1j).real
-    print(f"w256h9 oracle hessian {time.time() - t0:.1f}s  max|H| {np.abs(H).max():.3e} "
+    print(f"w256h{Nt} oracle hessian {time.time() - t0:.1f}s  max|H| {np.abs(H).max():.3e} "
           f"max|g| {np.abs(g).max():.3e} F {F}", flush=True)
-    np.savez_compressed(os.path.join(HERE, "c4_w256h9.npz"), u=u, H=H, grad=g, divT=divT, F=np.array([F]))
+    np.savez_compressed(os.path.join(HERE, f"c4_w256h{Nt}.npz"), u=u, H=H, grad=g, divT=divT, F=np.array([F]))
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["w256h9"]:
-        make_w256h9()
+    if len(sys.argv) == 2 and sys.argv[1].startswith("w256h") and sys.argv[1][5:].isdigit():
+        os.environ["ORC_HEEV"] = "ql"   # read by the oracle library at its first decomposition
+        make_w256hN(int(sys.argv[1][5:]))
         sys.exit(0)
     which = sys.argv[1:] or ["s32", "w256"]
     out = load_out()

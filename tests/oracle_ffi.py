@@ -42,6 +42,7 @@ def lib():
         L.orc_overlap_dH.argtypes = [C.c_void_p, ip, dp, ip, dp, dp]
         L.orc_apply_dH.argtypes = [C.c_void_p, ip, dp, ip, dp, C.c_size_t, C.POINTER(C.c_size_t)]
         L.orc_heev.argtypes = [C.c_int, dp, dp, dp]
+        L.orc_heev_ql.argtypes = [C.c_int, dp, dp, dp]
         L.orc_truncate.argtypes = [dp, C.c_int, C.c_double, C.c_int]
         L.orc_truncate.restype = C.c_int
         L.orc_oc_new.restype = C.c_void_p
@@ -228,6 +229,15 @@ def heev(A):
     a = np.ascontiguousarray(A, dtype=np.complex128)
     w = np.zeros(n); v = np.zeros(2 * n * n)
     lib().orc_heev(n, a.view(np.float64).ctypes.data_as(dp), w.ctypes.data_as(dp), v.ctypes.data_as(dp))
+    return w, v.view(np.complex128).reshape(n, n)
+
+
+def heev_ql(A):
+    """the oracle's Householder + QL solver (ORC_HEEV=ql) on one block"""
+    n = A.shape[0]
+    a = np.ascontiguousarray(A, dtype=np.complex128)
+    w = np.zeros(n); v = np.zeros(2 * n * n)
+    lib().orc_heev_ql(n, a.view(np.float64).ctypes.data_as(dp), w.ctypes.data_as(dp), v.ctypes.data_as(dp))
     return w, v.view(np.complex128).reshape(n, n)
 
 

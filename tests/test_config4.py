@@ -303,17 +303,23 @@ def test_c4_w256_hessian_vs_oracle(c4, warm256, monkeypatch, pipe):
     eng.close()
 
 
+def _long_fixtures():
+    import glob
+    return sorted(glob.glob(os.path.join(HERE, "golden", "c4_w256h[0-9]*.npz")))
+
+
 @pytest.mark.parametrize("pipe", ["1", "0"])
-def test_c4_w256_hessian9_vs_oracle(c4, warm256, monkeypatch, pipe):
-    """config 4's real bond dimension at N_t = 9 (7 rows, up to 6 row steps: the
-    pipelined path's row joins over more rows than w256h's 3): gradient, divT,
-    F and the full fidelity Hessian against the oracle (tests/golden/
-    make_c4_fixtures.py w256h9, ~3 h on the CPU restatement) at the north_star
-    tolerances, through the pipelined and the stored getHessian"""
+@pytest.mark.parametrize("path", _long_fixtures() or ["missing"], ids=os.path.basename)
+def test_c4_w256_hessian_long_vs_oracle(c4, warm256, monkeypatch, pipe, path):
+    """config 4's real bond dimension over a longer horizon (c4_w256h17.npz:
+    N_t = 17, 15 rows of up to 14 row steps: the pipelined path's row joins
+    over many more rows than w256h's 3): gradient, divT, F and the full
+    fidelity Hessian against the oracle (tests/golden/make_c4_fixtures.py
+    w256h17, the oracle with the Householder + QL eigensolver) at the
+    north_star tolerances, through the pipelined and the stored getHessian"""
     from optimalcontrolmps_amd.native import Engine
-    path = os.path.join(HERE, "golden", "c4_w256h9.npz")
     if not os.path.exists(path):
-        pytest.skip("w256h9 oracle fixture not generated")
+        pytest.skip("long-horizon w256 oracle fixture not generated")
     z = dict(np.load(path, allow_pickle=False))
     monkeypatch.setenv("OCG_HBM_PIPE", pipe)
     eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")

@@ -148,3 +148,24 @@ def test_hessian_formula_first_order_in_dt():
         gaps.append(gap)
     assert 0.02 < gaps[0] < 0.05           # 3.7 % at dt = 0.01
     assert 0.25 < gaps[1] / gaps[0] < 0.6  # 1.4 % at dt = 0.005
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 64, 160])
+def test_heev_ql_vs_numpy_and_jacobi(n):
+    """the oracle's Householder + QL eigensolver (ORC_HEEV=ql: zheev's
+    algorithm, used to generate the large chi fixtures) against numpy and the
+    default cyclic Jacobi on PSD Gram blocks with a spectrum spread over
+    twelve orders (the density matrices denmatDecomp diagonalises)"""
+    rng = np.random.default_rng(n)
+    X = rng.normal(size=(n, n + 2)) + 1j * rng.normal(size=(n, n + 2))
+    X *= np.logspace(0, -6, n)[:, None]
+    A = X @ X.conj().T
+    w, V = O.heev_ql(A)
+    wj, Vj = O.heev(A)
+    wn = np.sort(np.linalg.eigvalsh(A))[::-1]
+    scale = np.abs(wn).max()
+    assert np.all(np.diff(w) <= 0)
+    assert np.abs(w - wn).max() <= 1e-14 * scale * max(1, n / 16)
+    assert np.abs(w - wj).max() <= 1e-14 * scale * max(1, n / 16)
+    assert np.abs(V.conj().T @ V - np.eye(n)).max() <= 1e-13
+    assert np.abs(A @ V - V * w).max() <= 1e-14 * scale * max(1, n / 16)
