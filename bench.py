@@ -670,6 +670,8 @@ def bench_c4(args):
                                        limiter="the per-sector Hermitian eigensolver (k_heev_*) sets the step time; "
                                                "k_gemm launches are small (tasks of m, n ~ 16-60) and latency-bound"),
         }
+        if world == 1 and not args.no_cpu_baseline and not c5 and not grad and not args.profiled:
+            res["cpu_baseline"] = cpu_baseline_c4(ini, tgt, Nt, args.cpu_threads)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
@@ -688,6 +690,41 @@ def measured_traffic(kernel, tag="r01"):
             return json.load(f)["pmc_per_dispatch"][kernel]["hbm_bytes"]
     except (OSError, KeyError, ValueError):
         return None
+
+
+def cpu_baseline_c4(ini, tgt, Nt, threads):
+    """Config 4 on the CPU restatement (oracle/, 'port'), a bounded sample: one
+    chi = 256 step of the bench's own chain (L=20, p=7, from psi_init at U 2.5 ->
+    3.0) on one host thread, with the oracle's Householder + QL block
+    eigensolver (ORC_HEEV=ql: LAPACK zheev's algorithm, as ITensor's
+    diagHermitian; the default cyclic Jacobi takes ~14x longer).  The getHessian
+    of this slice is then priced from that step: psi and xi (2 (N_t - 1) steps on
+    two threads, calcPsiXiDivT), xiH (N_t dH applications, ~2 steps each, over
+    the threads) and the rows' (N_t-2)(N_t-3)/2 steps over the threads, as the
+    reference's calcHessian_parallel schedules them; value = rows/s of that
+    estimate at the threads available (measured: the step)."""
+    os.environ["ORC_HEEV"] = "ql"   # read at the oracle's first decomposition in this process
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    c = C4
+    L, p, Q = c["L"], c["p"], c["npart"]
+    st = O.Stepper(L, p, Q, c["J"], c["tstep"], c["cutoff"], c["maxm"])
+    psi0 = O.MPS(L, p, Q, ini.dims, ini.data)
+    t0 = time.perf_counter()
+    st.step(psi0, 2.5, 3.0, True)
+    t_step = time.perf_counter() - t0
+    avail = cpu_threads_available()
+    th = max(1, min(threads, avail)) if threads else avail
+    rows = Nt - 2
+    row_steps = rows * (rows - 1) // 2
+    est = t_step * ((Nt - 1) + 2.0 * Nt / th + (row_steps + 2.0 * rows) / th)
+    return {"value": rows / est, "unit": "rows/s", "cores": th, "kind": "port", "estimated": True,
+            "measured_step_s": t_step, "measured_sweep_steps_per_sec_1thread": 1.0 / t_step,
+            "host_threads_available": avail, "nproc": os.cpu_count(),
+            "sample": f"one chi=256 step of this chain on the C++ CPU restatement (oracle/, not ITensor; Householder "
+                      f"+ QL block eigensolver) on one thread, {t_step:.1f} s; the N_t={Nt} getHessian priced from it "
+                      f"at {th} threads (psi || xi serial, xiH and rows over the threads; the overlaps are not priced, "
+                      f"so the estimate favours the CPU)"}
 
 
 def cpu_threads_available():

@@ -1,0 +1,47 @@
+"""chi = 512 fixture (TEST INFRASTRUCTURE): config 5's local dimension and
+time step (p = 9, tstep = 0.01, cutoff 1e-8) at Maxm 512 on a chain short
+enough for the CPU oracle, L = 12, Npart = 12.  The Mott state |1..1> is
+evolved at U = 2.5 by the oracle (Householder + QL block eigensolver,
+ORC_HEEV=ql) until its middle bonds saturate at 512, then one oracle step
+u 2.5 -> 3.0 forward gives the bond dimensions, <psi_0|psi_1> and
+<psi_1|dH|psi_1> (as the w256 fixture does at config 4).
+Writes tests/golden/c5_w512.npz.  Run: python tests/golden/make_c5w512_fixture.py
+(hours on one core; progress and a resumable checkpoint in /tmp)."""
+import os
+import sys
+import time
+
+os.environ["ORC_HEEV"] = "ql"
+import numpy as np  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+import oracle_ffi as O  # noqa: E402
+from optimalcontrolmps_amd.states import product_state  # noqa: E402
+
+L, p, N, J, DT, CUT, MAXM = 12, 9, 12, 1.0, 0.01, 1e-8, 512
+CKPT = "/tmp/c5w512_ckpt.npz"
+
+if __name__ == "__main__":
+    st = O.Stepper(L, p, N, J, DT, CUT, MAXM)
+    if os.path.exists(CKPT):
+        z = np.load(CKPT, allow_pickle=False)
+        psi, steps = O.MPS(L, p, N, z["dims"], z["data"]), int(z["steps"])
+    else:
+        mott = product_state(L, p, N)
+        psi, steps = O.MPS(L, p, N, mott.dims, mott.data), 0
+    t0 = time.time()
+    while (np.asarray(psi.bond_dims()) == MAXM).sum() < 3 and steps < 800:
+        psi = st.steps(psi, np.full(11, 2.5), True)
+        steps += 10
+        np.savez(CKPT, dims=psi.dims, data=psi.data, steps=steps)
+        print(f"{steps} steps {time.time() - t0:.0f} s bonds {list(psi.bond_dims())}", flush=True)
+    t0 = time.time()
+    psi1 = st.steps(psi, np.array([2.5, 3.0]), True)
+    ov = st.overlap(psi, psi1)
+    dh = st.overlap_dH(psi1, psi1)
+    print(f"w512 oracle step {time.time() - t0:.1f}s bonds {list(psi1.bond_dims())} <0|1> {ov} <1|dH|1> {dh}",
+          flush=True)
+    np.savez_compressed(os.path.join(HERE, "c5_w512.npz"), dims=psi.dims, data=psi.data, steps=np.array(steps),
+                        bonds1=np.asarray(psi1.bond_dims()), ov01=np.array([ov]), dH11=np.array([dh]))

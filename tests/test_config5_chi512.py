@@ -174,3 +174,37 @@ def test_c5_w512_certified_vs_eigen_gauge(warm512, monkeypatch):
     assert abs(e1.overlap(s1, s1) - 1.0) <= 1e-12
     e1.close()
     e0.close()
+
+
+def test_c5_w512_L12_step_vs_oracle():
+    """an oracle pin at chi = 512 (tests/golden/c5_w512.npz, made by
+    tests/golden/make_c5w512_fixture.py): config 5's local dimension and
+    time step on a 12-site chain the CPU oracle can step, its middle bonds
+    saturated at Maxm 512 by the oracle itself; one GPU step u 2.5 -> 3.0
+    against the oracle's (bond dimensions, <psi_0|psi_1>, <psi_1|dH|psi_1>),
+    as test_c4_w256_step_vs_oracle does at config 4, on the default routing
+    (Gram orders up to 512 on the blocked eigensolver) and with every order
+    >= 65 on the blocked kernels"""
+    import os
+    from optimalcontrolmps_amd.native import MPS, Engine
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_w512.npz")
+    if not os.path.exists(path):
+        pytest.skip("chi = 512 oracle fixture not generated")
+    z = dict(np.load(path, allow_pickle=False))
+    Lx, Nx = 12, 12
+    psi0 = MPS(Lx, p, Nx, z["dims"], z["data"])
+    assert psi0.bond_dims().max() == MAXM
+    for bigmin in (None, "65"):
+        if bigmin:
+            os.environ["OCG_HBM_BIGMIN"] = bigmin
+        try:
+            eng = Engine(Lx, p, Nx, J, DT, CUT, MAXM, engine="hbm")
+            psi1 = eng.steps(psi0, np.array([2.5, 3.0]), True)
+            assert list(psi1.bond_dims()) == list(z["bonds1"])
+            assert abs(eng.overlap(psi0, psi1) - complex(z["ov01"][0])) <= 1e-10
+            dh = eng.overlap(psi1, psi1, True)
+            assert abs(dh - complex(z["dH11"][0])) <= 1e-9 * abs(complex(z["dH11"][0]))
+            assert abs(eng.overlap(psi1, psi1) - 1.0) <= 1e-12
+            eng.close()
+        finally:
+            os.environ.pop("OCG_HBM_BIGMIN", None)
