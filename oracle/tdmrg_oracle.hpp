@@ -27,6 +27,7 @@
 #include <cmath>
 #include <complex>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <limits>
 #include <mutex>
@@ -179,15 +180,20 @@ inline void heev_ql(int n, std::vector<cplx> A, std::vector<double>& w, std::vec
   std::vector<double> Z(size_t(n) * n, 0.0);
   for (int i = 0; i < n; ++i) Z[size_t(i) * n + i] = 1.0;
   const double eps = std::numeric_limits<double>::epsilon();
+  double tnorm = 0;
+  for (int i = 0; i < n; ++i) tnorm = std::max(tnorm, std::fabs(d[i]) + e[i] + (i ? e[i - 1] : 0.0));
+  // deflation: |e_m| negligible next to its diagonal neighbours, or below
+  // eps^2 ||T|| (graded Gram blocks with exactly singular tails: neighbours ~ 0)
+  const double floor_abs = eps * eps * tnorm;
   for (int l = 0; l < n; ++l) {
     int iter = 0, m;
     for (;;) {
       for (m = l; m + 1 < n; ++m) {
         const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
-        if (std::fabs(e[m]) <= eps * dd) break;
+        if (std::fabs(e[m]) <= eps * dd || std::fabs(e[m]) <= floor_abs) break;
       }
       if (m == l) break;
-      if (++iter > 200) throw std::runtime_error("heev_ql: no convergence");
+      if (++iter > 300) throw std::runtime_error("heev_ql: no convergence");
       double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
       double r = std::hypot(g, 1.0);
       g = d[m] - d[l] + e[l] / (g + (g >= 0 ? r : -r));
@@ -249,8 +255,15 @@ inline bool heev_use_ql() {
   return q;
 }
 inline void heev(int n, std::vector<cplx> A, std::vector<double>& w, std::vector<cplx>& V) {
-  if (heev_use_ql()) heev_ql(n, std::move(A), w, V);
-  else heev_jacobi(n, std::move(A), w, V);
+  if (heev_use_ql()) {
+    try {
+      heev_ql(n, A, w, V);
+      return;
+    } catch (const std::runtime_error&) {  // a block QL cannot deflate: the Jacobi solver takes it
+      std::fprintf(stderr, "[oracle] heev_ql did not converge on a block of order %d; cyclic Jacobi instead\n", n);
+    }
+  }
+  heev_jacobi(n, std::move(A), w, V);
 }
 
 // ---------------------------------------------------------------------------

@@ -11,8 +11,8 @@ tests at the reference's tolerances plus path equalities:
 * the analytic gradient vs central differences of the cost
   (tests/GradientTests.cpp:140-143: 0.1 %),
 * the interior fidelity Hessian vs central differences of the analytic
-  gradient: same signs, within 3 % (the reference formula is first order in
-  dt and compresses dH psi to Maxm; see test_c5_w512_hessian_fd),
+  gradient: to 1e-5 when Maxm does not bind (Maxm 1024), same signs and
+  within 3 % at config 5's binding Maxm 512 (see test_c5_w512_hessian_fd),
 * batched steps == single steps, pipelined getHessian == stored two-phase
   getHessian, bit for bit,
 * certified CholeskyQR2 gauge moves vs the eigen path: same bond dimensions,
@@ -83,11 +83,11 @@ def test_c5_w512_gradient_fd(warm512):
     eng.close()
 
 
-def _hessian_fd_gap(ini, tgt, u, dt):
+def _hessian_fd_gap(ini, tgt, u, dt, maxm=MAXM):
     """max over the interior of |H - dg/du| / |dg/du|: the fused getHessian
     against central differences of the analytic gradient, at time step dt"""
     from optimalcontrolmps_amd.native import Engine
-    eng = Engine(L, p, N, J, dt, CUT, MAXM, engine="hbm")
+    eng = Engine(L, p, N, J, dt, CUT, maxm, engine="hbm")
     eng.set_states(tgt, ini)
     H, divT, F = eng.hessian(u)
     assert np.array_equal(H, H.T)
@@ -111,24 +111,24 @@ def _hessian_fd_gap(ini, tgt, u, dt):
 
 
 def test_c5_w512_hessian_fd(warm512):
-    """calcHessianRow's entries (src/OptimalControl.cpp:251-279) are not the
-    exact derivative of the analytic gradient: they take d psi_j / d u_i to
-    first order in dt (on the CPU oracle at config 4's chain, Maxm 32, the gap
-    is 1.2-1.6 % at dt = 0.005 and 3.3-4.2 % at dt = 0.01,
-    tests/test_oracle.py::test_hessian_formula_first_order_in_dt), and with
-    Maxm binding the dH psi_i row states are compressed to Maxm like every
-    other exactApplyMPO (:256).  HessianTests' 5e-3 holds only at the
-    reference's own L = 5 test shape.  Here (chi = 512, MI355X): 1.4 % at
-    dt = 0.01 and 1.8 % at dt = 0.005 (tools/c5_hess_diag.py separates the
-    two sources); the test pins every interior entry's sign and a gap below
-    3 % at both time steps, against a gross error (factor, index, sign)."""
+    """calcHessianRow's entries (src/OptimalControl.cpp:251-279) differentiate
+    the propagation with the truncation held fixed.  From the chi = 512 state:
+    at Maxm 1024 (the bond-doubled dH psi_i and the grown trajectories are not
+    compressed) the fused Hessian equals central differences of the analytic
+    gradient to 1e-5 (measured 1e-5..3.5e-5, asserted < 1e-3); at config 5's
+    Maxm 512, which binds, the truncation the analytic derivative ignores
+    leaves 1.4 % (asserted < 3 %, every entry's sign) -- the reference's own
+    behaviour, as the oracle shows at smaller chains
+    (tests/test_oracle.py::test_hessian_vs_gradient_derivative_truncation).
+    HessianTests' 5e-3 (tests/HessianTests.cpp:178-205) is met wherever Maxm
+    does not bind."""
     ini, tgt = warm512
     u = np.random.default_rng(51).uniform(2.0, 10.0, NT)
-    g1 = _hessian_fd_gap(ini, tgt, u, DT)
-    g2 = _hessian_fd_gap(ini, tgt, u, DT / 2)
-    print(f"[c5 w512] Hessian vs FD of the gradient: {g1:.4f} at dt={DT}, {g2:.4f} at dt={DT / 2}")
-    assert g1 < 0.03
-    assert g2 < 0.03
+    g_bind = _hessian_fd_gap(ini, tgt, u, DT)
+    g_free = _hessian_fd_gap(ini, tgt, u, DT, maxm=2 * MAXM)
+    print(f"[c5 w512] Hessian vs FD of the gradient: {g_bind:.4f} at Maxm {MAXM}, {g_free:.2e} at Maxm {2 * MAXM}")
+    assert g_bind < 0.03
+    assert g_free < 1e-3
 
 
 def test_c5_w512_batched_equals_single(warm512):

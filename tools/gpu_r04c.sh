@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 4: full GPU suite, default bench line, population-exact profiles c4 (N_t=129) and c5 (N_t=17)
+# round 4: full GPU suite, default bench line, A/B of this round's library (A) against the
+# round-start build (ab/libprev.so, B) on config 1 and the c4rows slice, c4rows line with its CPU baseline
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -9,8 +10,12 @@ tail -2 gpurun_out/r04c_tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 300 python -u bench.py > gpurun_out/r04c_bench.json 2> gpurun_out/r04c_bench.err || { tail -20 gpurun_out/r04c_bench.err; exit 1; }
 cut -c1-300 gpurun_out/r04c_bench.json
-timeout -k 10 300 python -u tools/c5_warm_L12.py > gpurun_out/r04c_warmL12.log 2>&1 || { tail -5 gpurun_out/r04c_warmL12.log; exit 1; }
-tail -3 gpurun_out/r04c_warmL12.log
-timeout -k 10 900 bash tools/profile_r04.sh c4l c5 > gpurun_out/r04c_prof.log 2>&1 || { tail -20 gpurun_out/r04c_prof.log; exit 1; }
-tail -12 gpurun_out/r04c_prof.log
+timeout -k 10 300 python -u bench.py --workload c4rows --steps 3 --warmup 1 --state-cache /tmp/c4.npz > gpurun_out/r04c_c4rows.json 2> gpurun_out/r04c_c4rows.err || { tail -20 gpurun_out/r04c_c4rows.err; exit 1; }
+cut -c1-300 gpurun_out/r04c_c4rows.json
+for v in A B A B; do
+  if [ $v = B ]; then export OCG_LIB=$PWD/ab/libprev.so; else unset OCG_LIB; fi
+  timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 20 --warmup 2 > gpurun_out/r04c_ab1_$v.json 2>/dev/null || exit 1
+  timeout -k 10 300 python -u bench.py --workload c4rows --steps 3 --warmup 1 --no-cpu-baseline --state-cache /tmp/c4.npz > gpurun_out/r04c_ab4_$v.json 2>/dev/null || exit 1
+  python -c "import json; a=json.load(open('gpurun_out/r04c_ab1_$v.json')); b=json.load(open('gpurun_out/r04c_ab4_$v.json')); print('$v', 'c1', round(a['ms_per_step'],3), 'ms', 'c4rows', round(b['ms_per_step'],1), 'ms')"
+done
 exit $rc
