@@ -183,8 +183,10 @@ inline void heev_ql(int n, std::vector<cplx> A, std::vector<double>& w, std::vec
   double tnorm = 0;
   for (int i = 0; i < n; ++i) tnorm = std::max(tnorm, std::fabs(d[i]) + e[i] + (i ? e[i - 1] : 0.0));
   // deflation: |e_m| negligible next to its diagonal neighbours, or below
-  // eps^2 ||T|| (graded Gram blocks with exactly singular tails: neighbours ~ 0)
-  const double floor_abs = eps * eps * tnorm;
+  // eps ||T||: zheev's absolute accuracy (eigenvalues to ~eps ||A||), which the
+  // truncation (relative cutoffs >= 1e-14 of the total weight) never resolves
+  // below; without it graded blocks with tiny trailing eigenvalues stagnate
+  const double floor_abs = eps * tnorm;
   for (int l = 0; l < n; ++l) {
     int iter = 0, m;
     for (;;) {
