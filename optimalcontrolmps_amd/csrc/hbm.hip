@@ -642,10 +642,7 @@ struct Engine {
     hipEvent_t a = get_event(), b = get_event();
     // start / stop events of the dispatch itself (not stream markers around it: with the
     // host building the next launch's tasks the stream idles between a marker and the kernel)
-    // OCG_HBM_GEMM_PD=2|4: operand chunks in flight per segment (A/B; bitwise equal)
-    static const int gemm_pd = std::getenv("OCG_HBM_GEMM_PD") ? std::atoi(std::getenv("OCG_HBM_GEMM_PD")) : 1;
-    auto kg = gemm_pd >= 4 ? k_gemm_pd4 : gemm_pd == 2 ? k_gemm_pd2 : k_gemm;
-    hipExtLaunchKernelGGL(kg, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, dmap, ds, xcd_map ? 1 : 0);
+    hipExtLaunchKernelGGL(k_gemm, dim3(tiles), dim3(NT), 0, st, a, b, 0, dt_, dmap, ds, xcd_map ? 1 : 0);
     HCK(hipGetLastError());
     gemm_ev.push_back({a, b});
     ++gemm_launches;

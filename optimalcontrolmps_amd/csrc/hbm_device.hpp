@@ -119,14 +119,8 @@ constexpr int GT = 32, GK = 16;
 // MI355X_MICROARCH.md §Workgroup dispatch) take consecutive tiles, so a task's
 // tiles share that XCD's L2 for their common operand rows / columns (speed
 // only: any bijection of workgroups onto tiles computes the same result)
-// PD: operand chunks in flight.  PD = 1 stages chunk c while chunk c + 1 loads;
-// PD > 1 issues the loads of the first PD chunks of a segment at once and
-// refills a slot as soon as it is staged, so a segment of k <= PD GK costs one
-// global round trip instead of k / GK (more registers: 16 VGPRs per slot).
-// Every PD computes the same MFMA sequence, so the results are bitwise equal.
-template <int PD>
-__device__ __forceinline__ void gemm_body(const GTask* __restrict__ tasks, const int2* __restrict__ tile_task,
-                                          const GSeg* __restrict__ segs, int xcd) {
+__global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, const int2* __restrict__ tile_task,
+                                             const GSeg* __restrict__ segs, int xcd) {
   constexpr int EA = GT * GK / NT;  // staged elements per thread and operand
   __shared__ double Ar[GT][GK + 1], Ai[GT][GK + 1], Br[GK][GT + 1], Bi[GK][GT + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -154,9 +148,9 @@ __device__ __forceinline__ void gemm_body(const GTask* __restrict__ tasks, const
   for (int s = 0; s < T.nseg; ++s) {
     const GSeg S = s == 0 ? S0 : segs[T.seg0 + s];
     const bool ca = S.ops & 1, cb = (S.ops >> 1) & 1;
-    // global -> registers for the chunk at k0 (issued ahead of its MFMAs)
-    z va[PD][EA], vb[PD][EA];
-    auto gload = [&](int k0, z* ra, z* rb) {
+    // global -> registers for the chunk at k0 (issued one chunk ahead of its MFMAs)
+    z va[EA], vb[EA];
+    auto gload = [&](int k0) {
 #pragma unroll
       for (int t = 0; t < EA; ++t) {
         const int e = tid + NT * t;
@@ -170,7 +164,7 @@ __device__ __forceinline__ void gemm_body(const GTask* __restrict__ tasks, const
           if (ca) v.y = -v.y;
           v = zsc(v, S.alpha);
         }
-        ra[t] = v;
+        va[t] = v;
       }
 #pragma unroll
       for (int t = 0; t < EA; ++t) {
@@ -184,44 +178,37 @@ __device__ __forceinline__ void gemm_body(const GTask* __restrict__ tasks, const
           v = cb ? S.B[(size_t)gc * S.ldb + gk] : S.B[(size_t)gk * S.ldb + gc];
           if (cb) v.y = -v.y;
         }
-        rb[t] = v;
+        vb[t] = v;
       }
     };
+    if (S.k > 0) gload(0);
+    for (int k0 = 0; k0 < S.k; k0 += GK) {
+      // stage op(A)[m0.., k0..] (32 x GK) and op(B)[k0.., n0..] (GK x 32)
 #pragma unroll
-    for (int c = 0; c < PD; ++c)
-      if (c * GK < S.k) gload(c * GK, va[c], vb[c]);
-    for (int kb = 0; kb < S.k; kb += PD * GK) {
-#pragma unroll
-      for (int c = 0; c < PD; ++c) {
-        const int k0 = kb + c * GK;
-        if (k0 >= S.k) break;  // uniform
-        // stage op(A)[m0.., k0..] (32 x GK) and op(B)[k0.., n0..] (GK x 32)
-#pragma unroll
-        for (int t = 0; t < EA; ++t) {
-          const int e = tid + NT * t;
-          const int r = !ca ? e / GK : e % GT, kk = !ca ? e % GK : e / GT;
-          Ar[r][kk] = va[c][t].x;
-          Ai[r][kk] = va[c][t].y;
-          const int kbb = !cb ? e / GT : e % GK, cc = !cb ? e % GT : e / GK;
-          Br[kbb][cc] = vb[c][t].x;
-          Bi[kbb][cc] = vb[c][t].y;
-        }
-        __syncthreads();
-        if (k0 + PD * GK < S.k) gload(k0 + PD * GK, va[c], vb[c]);
-#pragma unroll
-        for (int ks = 0; ks < GK; ks += 4) {
-          if (live && k0 + ks < S.k) {  // k-steps past the end would only add zeros
-            const int ar = wm + (lane & 15), kk = ks + (lane >> 4), bc = wn + (lane & 15);
-            const double are = Ar[ar][kk], aim = Ai[ar][kk];
-            const double bre = Br[kk][bc], bim = Bi[kk][bc];
-            cr = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bre, cr, 0, 0, 0);
-            cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-aim, bim, cr, 0, 0, 0);
-            ci = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bim, ci, 0, 0, 0);
-            ci = __builtin_amdgcn_mfma_f64_16x16x4f64(aim, bre, ci, 0, 0, 0);
-          }
-        }
-        __syncthreads();
+      for (int t = 0; t < EA; ++t) {
+        const int e = tid + NT * t;
+        const int r = !ca ? e / GK : e % GT, kk = !ca ? e % GK : e / GT;
+        Ar[r][kk] = va[t].x;
+        Ai[r][kk] = va[t].y;
+        const int kb = !cb ? e / GT : e % GK, c = !cb ? e % GT : e / GK;
+        Br[kb][c] = vb[t].x;
+        Bi[kb][c] = vb[t].y;
       }
+      __syncthreads();
+      if (k0 + GK < S.k) gload(k0 + GK);
+#pragma unroll
+      for (int ks = 0; ks < GK; ks += 4) {
+        if (live && k0 + ks < S.k) {  // k-steps past the end would only add zeros
+          const int ar = wm + (lane & 15), kk = ks + (lane >> 4), bc = wn + (lane & 15);
+          const double are = Ar[ar][kk], aim = Ai[ar][kk];
+          const double bre = Br[kk][bc], bim = Bi[kk][bc];
+          cr = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bre, cr, 0, 0, 0);
+          cr = __builtin_amdgcn_mfma_f64_16x16x4f64(-aim, bim, cr, 0, 0, 0);
+          ci = __builtin_amdgcn_mfma_f64_16x16x4f64(are, bim, ci, 0, 0, 0);
+          ci = __builtin_amdgcn_mfma_f64_16x16x4f64(aim, bre, ci, 0, 0, 0);
+        }
+      }
+      __syncthreads();
     }
   }
   const double sc = scale_of(T.sc, 0, (T.smode >> 4) & 3);
@@ -236,18 +223,6 @@ __device__ __forceinline__ void gemm_body(const GTask* __restrict__ tasks, const
       T.C[(size_t)row * T.ldc + col] = mk(cr[r] * f, ci[r] * f);
     }
   }
-}
-__global__ __launch_bounds__(NT) void k_gemm(const GTask* __restrict__ tasks, const int2* __restrict__ tile_task,
-                                             const GSeg* __restrict__ segs, int xcd) {
-  gemm_body<1>(tasks, tile_task, segs, xcd);
-}
-__global__ __launch_bounds__(NT) void k_gemm_pd2(const GTask* __restrict__ tasks, const int2* __restrict__ tile_task,
-                                                 const GSeg* __restrict__ segs, int xcd) {
-  gemm_body<2>(tasks, tile_task, segs, xcd);
-}
-__global__ __launch_bounds__(NT) void k_gemm_pd4(const GTask* __restrict__ tasks, const int2* __restrict__ tile_task,
-                                                 const GSeg* __restrict__ segs, int xcd) {
-  gemm_body<4>(tasks, tile_task, segs, xcd);
 }
 
 // ------------------------------------------------------------------ copies

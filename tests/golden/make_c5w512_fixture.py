@@ -6,7 +6,12 @@ ORC_HEEV=ql) until its middle bonds saturate at 512, then one oracle step
 u 2.5 -> 3.0 forward gives the bond dimensions, <psi_0|psi_1> and
 <psi_1|dH|psi_1> (as the w256 fixture does at config 4).
 Writes tests/golden/c5_w512.npz.  Run: python tests/golden/make_c5w512_fixture.py
-(hours on one core; progress and a resumable checkpoint in /tmp)."""
+(hours on one core; progress and a resumable checkpoint in /tmp).
+
+`... make_c5w512_fixture.py hess`: from that state (psi_init = psi_target =
+the saturated state, so no second state is stored), N_t = 5 GRAPE controls
+U(2,10) (seed 5512): divT, F, gradient and the full fidelity Hessian on the
+oracle with 8 threads -> tests/golden/c5_w512h.npz."""
 import os
 import sys
 import time
@@ -23,7 +28,26 @@ from optimalcontrolmps_amd.states import product_state  # noqa: E402
 L, p, N, J, DT, CUT, MAXM = 12, 9, 12, 1.0, 0.01, 1e-8, 512
 CKPT = "/tmp/c5w512_ckpt.npz"
 
+def make_hess():
+    z = np.load(os.path.join(HERE, "c5_w512.npz"), allow_pickle=False)
+    st = O.Stepper(L, p, N, J, DT, CUT, MAXM)
+    psi = O.MPS(L, p, N, z["dims"], z["data"])
+    Nt = 5
+    u = np.random.default_rng(5512).uniform(2.0, 10.0, Nt)
+    oc = O.OC(st, psi, psi, Nt, 0.0)
+    t0 = time.time()
+    H = oc.hessian(u, 8)
+    divT, F = oc.divT_F()
+    g = DT * (divT * F * 1j).real
+    print(f"w512h oracle hessian {time.time() - t0:.1f}s max|H| {np.abs(H).max():.3e} max|g| {np.abs(g).max():.3e} "
+          f"F {F}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "c5_w512h.npz"), u=u, H=H, grad=g, divT=divT, F=np.array([F]))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["hess"]:
+        make_hess()
+        sys.exit(0)
     st = O.Stepper(L, p, N, J, DT, CUT, MAXM)
     if os.path.exists(CKPT):
         z = np.load(CKPT, allow_pickle=False)

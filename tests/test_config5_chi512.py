@@ -208,3 +208,32 @@ def test_c5_w512_L12_step_vs_oracle():
             eng.close()
         finally:
             os.environ.pop("OCG_HBM_BIGMIN", None)
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_c5_w512_L12_hessian_vs_oracle(monkeypatch, pipe):
+    """the chi = 512 oracle pin of the derivatives (tests/golden/c5_w512h.npz,
+    make_c5w512_fixture.py hess): from the 12-site saturated state (psi_init =
+    psi_target), N_t = 5 GRAPE controls: divT, F, the gradient and the full
+    fidelity Hessian against the oracle at the north_star tolerances, through
+    the pipelined and the stored getHessian"""
+    import os
+    from optimalcontrolmps_amd.native import MPS, Engine
+    gd = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    if not (os.path.exists(os.path.join(gd, "c5_w512.npz")) and os.path.exists(os.path.join(gd, "c5_w512h.npz"))):
+        pytest.skip("chi = 512 oracle Hessian fixture not generated")
+    zs = dict(np.load(os.path.join(gd, "c5_w512.npz"), allow_pickle=False))
+    z = dict(np.load(os.path.join(gd, "c5_w512h.npz"), allow_pickle=False))
+    Lx, Nx = 12, 12
+    psi = MPS(Lx, p, Nx, zs["dims"], zs["data"])
+    monkeypatch.setenv("OCG_HBM_PIPE", pipe)
+    eng = Engine(Lx, p, Nx, J, DT, CUT, MAXM, engine="hbm")
+    eng.set_states(psi, psi)
+    H, divT, F = eng.hessian(z["u"])
+    g = DT * (divT * F * 1j).real
+    Fo = complex(z["F"][0])
+    assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12
+    assert np.abs(divT - z["divT"]).max() <= 1e-8 * np.abs(z["divT"]).max()
+    assert np.abs(g - z["grad"]).max() <= 1e-6
+    assert np.abs(H - z["H"]).max() <= 1e-6 * np.abs(z["H"]).max()
+    eng.close()
