@@ -2636,10 +2636,12 @@ static double heap_growth_bytes(const hbm_engine* h, double slots) {
   return slots <= double(h->E->heap_slots) ? 0.0 : 16.0 * double(h->E->state_cap) * slots;
 }
 double hbm_traj_bytes(const hbm_engine* h, int N) { return heap_growth_bytes(h, 3.0 * N + 6.0); }
-// bytes a pool of n chains (with their share of the workspace, as hbm_batch
-// prices them) would newly allocate on an engine holding `have` chains
+// bytes a pool of n chains would newly allocate on an engine holding `have`
+// chains (the pool itself, 16 B per element, and half as much again for the
+// workspace arenas the chains' launches draw on); a call that still runs out
+// of memory fails cleanly and its caller takes the lighter path
 static double chain_growth_bytes(const hbm::Engine& E, int n, int have, bool wide) {
-  return n <= have ? 0.0 : 16.0 * 4.0 * double(E.chain_elems(wide)) * n;
+  return n <= have ? 0.0 : 16.0 * 1.5 * double(E.chain_elems(wide)) * n;
 }
 double hbm_gradient_multi_bytes(const hbm_engine* h, int K, int N) {
   const hbm::Engine& E = *h->E;

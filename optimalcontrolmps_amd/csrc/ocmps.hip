@@ -331,10 +331,10 @@ static int ensure_buf(ocg_ctx* c, T*& ptr, int& cap, int n) {
 static int ensure_pin(ocg_ctx* c, size_t bytes) {
   if (bytes <= c->pin_cap) return 0;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t m = std::max(bytes, 2 * c->pin_cap);
   if (c->h_pin) (void)hipHostFree(c->h_pin);
   c->h_pin = nullptr;
   c->pin_cap = 0;
-  const size_t m = std::max(bytes, 2 * c->pin_cap);
   HIPCHK(c, hipHostMalloc((void**)&c->h_pin, m, hipHostMallocDefault));
   c->pin_cap = m;
   return 0;
