@@ -274,6 +274,20 @@ struct Engine {
     if (st) (void)hipStreamDestroy(st);
   }
 
+  // stream priority: 1 high (the context engine, the dH worker: the rows'
+  // critical path), -1 low (the pipelined getHessian's xi worker, whose
+  // states are needed only by the closing overlap pass), 0 default.  Applied
+  // when OCG_HBM_PRIO=1 (A/B).
+  int prio_level = 0;
+  hipError_t create_stream(hipStream_t* s) const {
+    static const bool on = std::getenv("OCG_HBM_PRIO") && std::getenv("OCG_HBM_PRIO")[0] == '1';
+    if (on && prio_level != 0) {
+      int least = 0, greatest = 0;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio_level > 0 ? greatest : least);
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  }
   // ------------------------------------------------------------ setup
   void init(const std::vector<int>& md_in, const std::vector<int>& mdz_in, const std::vector<double>& gf,
             const std::vector<double>& gb, const int* glo, const int* gsz, const int* goff, int gtotal,
@@ -281,7 +295,7 @@ struct Engine {
     HCK(hipSetDevice(device));
     if (const char* e = std::getenv("OCG_HBM_REGMIN")) reg_min = std::max(2, std::atoi(e));
     thost.pinned = true;
-    HCK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HCK(create_stream(&st));
     HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
     {
       std::vector<z> I(size_t(kCholMax) * kCholMax, mk(0, 0));
@@ -878,7 +892,7 @@ struct Engine {
       const bool side = !big.empty() || !small.empty();
       if (side) {  // on the side stream, after everything st has queued (incl. this upload)
         if (!st2) {  // created on first use: every stream takes a hardware queue (GPU_MAX_HW_QUEUES)
-          HCK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+          HCK(create_stream(&st2));
           HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
           HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
         }
@@ -2211,6 +2225,7 @@ int hbm_create(int device, int L, int p, int npart, double J, double tstep, doub
                const std::vector<int>& gates, hbm_engine** out, std::string& err) {
   auto* h = new hbm_engine;
   h->E.reset(new hbm::Engine(device, L, p, npart, J, tstep, cutoff, maxm));
+  h->E->prio_level = 1;
   h->md = md;
   h->mdz = mdz;
   h->gates = gates;
@@ -2944,6 +2959,7 @@ hbm::Engine& pipe_worker(hbm_engine* h, int k) {
   if (W && (W->bcap != E.bcap || W->bcapw != E.bcapw)) W.reset();
   if (!W) {
     W.reset(new hbm::Engine(E.device, E.L, E.p, E.Q, E.J, E.dt, E.cutoff, E.maxm));
+    W->prio_level = k == 0 ? 1 : -1;
     W->init(h->md, h->mdz, h->gf, h->gb, h->glo, h->gsz, h->goff, h->gtotal, h->gates);
     W->set_caps(E.widest);
     if (W->bcap != E.bcap || W->bcapw != E.bcapw || W->state_cap != E.state_cap)
