@@ -276,11 +276,15 @@ struct Engine {
 
   // stream priority: 1 high (the context engine, the dH worker: the rows'
   // critical path), -1 low (the pipelined getHessian's xi worker, whose
-  // states are needed only by the closing overlap pass), 0 default.  Applied
-  // when OCG_HBM_PRIO=1 (A/B).
+  // states are needed only by the closing overlap pass), 0 default.  The
+  // three engines of the pipelined getHessian share the CUs; with the xi
+  // worker's launches behind the critical path's, c4rows 1976 -> 1688 ms and
+  // c5rows 15.1 -> 12.0 s per getHessian (same results bit for bit: the
+  // engines hand states over through counters).  OCG_HBM_PRIO=0: default
+  // priorities for every stream (A/B).
   int prio_level = 0;
   hipError_t create_stream(hipStream_t* s) const {
-    static const bool on = std::getenv("OCG_HBM_PRIO") && std::getenv("OCG_HBM_PRIO")[0] == '1';
+    static const bool on = !(std::getenv("OCG_HBM_PRIO") && std::getenv("OCG_HBM_PRIO")[0] == '0');
     if (on && prio_level != 0) {
       int least = 0, greatest = 0;
       if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
