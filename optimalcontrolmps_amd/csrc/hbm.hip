@@ -278,14 +278,18 @@ struct Engine {
   // critical path), -1 low (the pipelined getHessian's xi worker, whose
   // states are needed only by the closing overlap pass), 0 default.  The
   // three engines of the pipelined getHessian share the CUs; with the xi
-  // worker's launches behind the critical path's, c4rows 1976 -> 1688 ms and
-  // c5rows 15.1 -> 12.0 s per getHessian (same results bit for bit: the
-  // engines hand states over through counters).  OCG_HBM_PRIO=0: default
-  // priorities for every stream (A/B).
+  // worker's launches behind the critical path's the getHessian is faster
+  // (same results bit for bit: the engines hand states over through counters).
   int prio_level = 0;
   hipError_t create_stream(hipStream_t* s) const {
-    static const bool on = !(std::getenv("OCG_HBM_PRIO") && std::getenv("OCG_HBM_PRIO")[0] == '0');
-    if (on && prio_level != 0) {
+    // OCG_HBM_PRIO: 2 (default) the xi worker low, the others default; 1 also the
+    // context engine and the dH worker high; 0 every stream default.  Measured on
+    // c4rows (one box, two repetitions): 2 -> 1745-1750 ms whether the engine ran
+    // steps before its first getHessian or not; 1 -> 1681-1702 ms or 2069-2078 ms
+    // depending on that (the order in which the high-priority streams are created
+    // decides which of them share a hardware queue); 0 -> 1856-2200 ms.
+    static const int mode = std::getenv("OCG_HBM_PRIO") ? std::atoi(std::getenv("OCG_HBM_PRIO")) : 2;
+    if (mode != 0 && prio_level != 0 && !(mode == 2 && prio_level > 0)) {
       int least = 0, greatest = 0;
       if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
         return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio_level > 0 ? greatest : least);
