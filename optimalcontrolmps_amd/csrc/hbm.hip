@@ -281,7 +281,7 @@ struct Engine {
   // worker's launches behind the critical path's the getHessian is faster
   // (same results bit for bit: the engines hand states over through counters).
   int prio_level = 0;
-  hipError_t create_stream(hipStream_t* s) const {
+  hipError_t create_stream(hipStream_t* s, bool side = false) const {
     // OCG_HBM_PRIO: 2 (default) the xi worker low, the others default; 1 also the
     // context engine and the dH worker high; 0 every stream default.  Measured on
     // c4rows (one box, two repetitions): 2 -> 1745-1750 ms whether the engine ran
@@ -289,7 +289,9 @@ struct Engine {
     // depending on that (the order in which the high-priority streams are created
     // decides which of them share a hardware queue); 0 -> 1856-2200 ms.
     static const int mode = std::getenv("OCG_HBM_PRIO") ? std::atoi(std::getenv("OCG_HBM_PRIO")) : 2;
-    if (mode != 0 && prio_level != 0 && !(mode == 2 && prio_level > 0)) {
+    // mode 3: as 1, but an engine's side stream (st2) stays at the default priority
+    // when its main stream is high, so only two streams ever ask for high priority
+    if (mode != 0 && prio_level != 0 && !(mode == 2 && prio_level > 0) && !(mode == 3 && side && prio_level > 0)) {
       int least = 0, greatest = 0;
       if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
         return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio_level > 0 ? greatest : least);
@@ -900,7 +902,7 @@ struct Engine {
       const bool side = !big.empty() || !small.empty();
       if (side) {  // on the side stream, after everything st has queued (incl. this upload)
         if (!st2) {  // created on first use: every stream takes a hardware queue (GPU_MAX_HW_QUEUES)
-          HCK(create_stream(&st2));
+          HCK(create_stream(&st2, true));
           HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
           HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
         }
