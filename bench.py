@@ -56,6 +56,7 @@ CFG = dict(L=5, p=5, npart=5, J=1.0, tstep=0.01, T=2.0, maxm=80, cutoff=1e-8, U_
            seed=20261015)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFS = 78.6       # MI355X FP64 vector/matrix spec
+FP64_MFMA_MEASURED_TFS = 48.7   # v_mfma_f64_16x16x4f64 issue rate measured on the box (tools/mfma_f64_peak.hip)
 
 
 def parse_args(argv=None):
@@ -360,6 +361,7 @@ def roofline_block(kernel, launch_ms, bytes_per_launch, flops_per_launch, tag, l
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     traffic = measured_traffic(kernel, tag)
     meas = traffic / (launch_ms * 1e-3) / 1e9 if (traffic and launch_ms > 0) else None
+    tf = flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0
     return {
         "bound": bound,
         "limiter": limiter,
@@ -373,8 +375,10 @@ def roofline_block(kernel, launch_ms, bytes_per_launch, flops_per_launch, tag, l
         "measured_frac": (meas / HBM_PEAK_GBS) if meas is not None else None,
         "alg_bytes_per_launch": bytes_per_launch,
         "avg_launch_ms": launch_ms,
-        "fp64_achieved_tflops": flops_per_launch / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0,
+        "fp64_achieved_tflops": tf,
         "fp64_peak_tflops": FP64_PEAK_TFS,
+        "fp64_frac": tf / FP64_PEAK_TFS,
+        "fp64_mfma_measured_peak_tflops": FP64_MFMA_MEASURED_TFS,
     }
 
 
