@@ -282,15 +282,13 @@ struct Engine {
   // (same results bit for bit: the engines hand states over through counters).
   int prio_level = 0;
   hipError_t create_stream(hipStream_t* s, bool side = false) const {
-    // OCG_HBM_PRIO: 2 (default) the xi worker low, the others default; 1 also the
-    // context engine and the dH worker high; 0 every stream default.  Measured on
-    // c4rows (one box, two repetitions): 2 -> 1745-1750 ms whether the engine ran
-    // steps before its first getHessian or not; 1 -> 1681-1702 ms or 2069-2078 ms
-    // depending on that (the order in which the high-priority streams are created
-    // decides which of them share a hardware queue); 0 -> 1856-2200 ms.
-    static const int mode = std::getenv("OCG_HBM_PRIO") ? std::atoi(std::getenv("OCG_HBM_PRIO")) : 2;
-    // mode 3: as 1, but an engine's side stream (st2) stays at the default priority
-    // when its main stream is high, so only two streams ever ask for high priority
+    // OCG_HBM_PRIO: 3 (default) the main streams of the context engine and the dH
+    // worker high, their side streams default, both xi-worker streams low; 1 the
+    // side streams high as well; 2 only the xi worker low; 0 every stream default.
+    // Measured (round 4, one box per row, results bitwise the same in every mode):
+    // c4rows 3 -> 1670-1706 ms, 2 -> 1694-1758 ms, 0 -> 1856-2200 ms;
+    // c5rows 3 / 1 -> 11.99-12.28 s, 2 -> 15.94-15.98 s, 0 -> 15.12-20.79 s.
+    static const int mode = std::getenv("OCG_HBM_PRIO") ? std::atoi(std::getenv("OCG_HBM_PRIO")) : 3;
     if (mode != 0 && prio_level != 0 && !(mode == 2 && prio_level > 0) && !(mode == 3 && side && prio_level > 0)) {
       int least = 0, greatest = 0;
       if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
