@@ -287,7 +287,7 @@ struct Engine {
     // side streams high as well; 2 only the xi worker low; 0 every stream default.
     // Measured (round 4, one box per row, results bitwise the same in every mode):
     // c4rows 3 -> 1670-1706 ms, 2 -> 1694-1758 ms, 0 -> 1856-2200 ms;
-    // c5rows 3 / 1 -> 11.99-12.28 s, 2 -> 15.94-15.98 s, 0 -> 15.12-20.79 s.
+    // c5rows 3 / 1 -> 11.60-12.28 s, 2 -> 13.19-15.98 s, 0 -> 15.12-20.79 s.
     static const int mode = std::getenv("OCG_HBM_PRIO") ? std::atoi(std::getenv("OCG_HBM_PRIO")) : 3;
     if (mode != 0 && prio_level != 0 && !(mode == 2 && prio_level > 0) && !(mode == 3 && side && prio_level > 0)) {
       int least = 0, greatest = 0;
