@@ -41,12 +41,6 @@ import os
 import sys
 import time
 
-# Every HIP stream of this process gets its own hardware queue (the HIP default
-# is 4 per process): the pipelined HBM getHessian runs three engines on three
-# streams beside torch's, and streams that share a queue serialise each other
-# and stretch the dispatch events the roofline is timed with.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -86,11 +80,16 @@ def parse_args(argv=None):
     ap.add_argument("--multi", type=int, default=1,
                     help="K control vectors per GPU in one ocg_hessian_multi call (one pipeline launch for all K); "
                          "value = rows of all K per second")
-    ap.add_argument("--profile-tag", default="r04")
+    ap.add_argument("--profile-tag", default="r05")
     ap.add_argument("--profiled", action="store_true",
                     help="run only the warm-up and timed getHessian calls (no single-chain probe, no config-2 "
-                         "block): the command rocprofv3 profiles, so every dispatch of a kernel belongs to the "
-                         "population the roofline divides by")
+                         "block, no config-4 / config-5 slice blocks, no CPU baseline): the command rocprofv3 "
+                         "profiles, so every dispatch of a kernel belongs to the population the roofline divides by")
+    ap.add_argument("--no-slices", action="store_true",
+                    help="config 1 at N=1: skip the config-4 / config-5 slice blocks (child processes run before "
+                         "the config-1 line)")
+    ap.add_argument("--c4-cpu-nt", type=int, default=5,
+                    help="time points of the measured oracle getHessian in the c4rows CPU baseline (0: skip)")
     ap.add_argument("--multi-info", action="store_true",
                     help="after the timed region also time 8 Hessians / 64 gradients per call (ocg_*_multi; "
                          "their k_pipeline launches would enter a rocprofv3 summary of the command)")
@@ -172,14 +171,63 @@ def main(argv=None):
     args = parse_args(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus, argv)
-    return run(args)
+    blocks = None
+    if (args.workload == "hessian" and args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+            and not args.profiled and not args.no_slices and args.multi == 1 and args.controls == 1):
+        # before this process touches the GPU: the children start from a process
+        # that never made a HIP call (no exec of a GPU process, no fork of one)
+        blocks = slice_blocks(args)
+    return run(args, blocks)
 
 
 def run_argv(argv):
     return run(parse_args(argv))
 
 
-def run(args):
+SLICE_TIMEOUT_S = 420
+
+
+def slice_blocks(args):
+    """Configs 4 and 5 (BASELINE configs[3], configs[4]) in the default N=1 line:
+    each runs as `bench.py --workload c4rows|c5rows` in a fresh child interpreter
+    (its own HIP context; nothing of this process is inherited but the
+    environment), one after the other and before the config-1 measurement, so
+    no GPU work overlaps a timed region.  A failing or hung child leaves an
+    `error` field in its block and the headline line intact.  Harness model:
+    main/TestRuntimes.cpp:55-71 (getAnalyticGradient, then getHessian, each
+    timed)."""
+    import subprocess
+    me = os.path.abspath(__file__)
+    common = ["--gpus", "1", "--profile-tag", args.profile_tag, "--cpu-threads", str(args.cpu_threads)]
+    if args.no_cpu_baseline:
+        common.append("--no-cpu-baseline")
+    jobs = [("config4_slice", ["--workload", "c4rows", "--c4-nt", "33", "--steps", "2", "--warmup", "1",
+                               "--c4-cpu-nt", str(args.c4_cpu_nt)]),
+            ("config5_slice", ["--workload", "c5rows", "--c5-nt", "17", "--steps", "1", "--warmup", "1"])]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    out = {}
+    for name, extra in jobs:
+        t0 = time.perf_counter()
+        print(f"[bench] {name}: child bench.py {' '.join(extra)}", file=sys.stderr, flush=True)
+        try:
+            cp = subprocess.run([sys.executable, "-u", me] + extra + common, stdout=subprocess.PIPE, stderr=None,
+                                text=True, timeout=SLICE_TIMEOUT_S, env=env, cwd=ROOT)
+            lines = [ln for ln in cp.stdout.splitlines() if ln.startswith("{")]
+            if cp.returncode != 0 or not lines:
+                out[name] = {"error": f"child exited {cp.returncode}", "stdout_tail": cp.stdout[-2000:]}
+            else:
+                out[name] = json.loads(lines[-1])
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": f"child timed out after {SLICE_TIMEOUT_S} s"}
+        except (OSError, ValueError) as e:
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+        out[name]["child_wall_s"] = time.perf_counter() - t0
+        print(f"[bench] {name}: {out[name]['child_wall_s']:.0f} s", file=sys.stderr, flush=True)
+    return out
+
+
+def run(args, blocks=None):
     if args.workload in ("c4grad", "c4rows", "c5rows"):
         return bench_c4(args)
 
@@ -266,9 +314,11 @@ def run(args):
     st_rows = eng.stats(5)       # k_pipeline: trajectories + row re-propagation (dominant)
     st_ovl = eng.stats(6)        # k_row_overlaps
     st_div = eng.stats(1)        # divT / F overlaps
-    t_tr = time.perf_counter()
-    eng.propagate(u, 3)          # one bare psi || xi trajectory (outside the timed region): single-chain step rate
-    t_tr = time.perf_counter() - t_tr
+    t_tr = None
+    if not args.profiled:        # a profiled command holds only the timed population
+        t_tr = time.perf_counter()
+        eng.propagate(u, 3)      # one bare psi || xi trajectory (outside the timed region): single-chain step rate
+        t_tr = time.perf_counter() - t_tr
     # throughput with several control vectors per call (IPOPT trial points, FD probes,
     # multi-start), outside the timed region: reported beside `value`, never as it
     multi_info = None
@@ -321,24 +371,36 @@ def run(args):
                 "row_overlaps": {"avg_ms": st_ovl["ms"] / max(1, st_ovl["launches"]), "launches": st_ovl["launches"]},
                 "divT_F_overlaps_ms": st_div["ms"] / max(1, args.steps),
             },
-            "single_chain_steps_per_sec": (Nt - 1) / t_tr,
+            "single_chain_steps_per_sec": (Nt - 1) / t_tr if t_tr else None,
             "multi_control": multi_info,
             "roofline": roofline_block("k_pipeline", launch_ms, bytes_per_launch, flops_per_launch,
                                        args.profile_tag,
                                        limiter="issue latency: one chain's N_t-1 dependent steps on one CU "
                                                "(state in LDS); HBM and FP64 are both <1% busy", bound="latency"),
         }
+        result["env"] = run_env()
         # config 2 (BASELINE configs[1]) after the timed region, as main/TestRuntimes.cpp:55-63
         # times getAnalyticGradient before getHessian
-        result["config2_gradient"] = config2_gradient(eng, u, Nt, dt, args.profile_tag,
-                                                      cpu=(world == 1 and not args.no_cpu_baseline),
-                                                      ini=ini, tgt=tgt)
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.profiled:
+            result["config2_gradient"] = config2_gradient(eng, u, Nt, dt, args.profile_tag,
+                                                          cpu=(world == 1 and not args.no_cpu_baseline),
+                                                          ini=ini, tgt=tgt)
+        if world == 1 and not args.no_cpu_baseline and not args.profiled:
             result["cpu_baseline"] = cpu_baseline(ini, tgt, u, args.cpu_threads)
+        if blocks:   # configs 4 and 5, measured in child processes before this line's timed region
+            result.update(blocks)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_env():
+    """the run-time settings a line's numbers depend on, read back from this
+    process's environment (GPU_MAX_HW_QUEUES: hardware queues per process, HIP's
+    default 4 when unset; the GPU box exports 4)"""
+    keys = ("GPU_MAX_HW_QUEUES", "OMP_NUM_THREADS", "OCG_HBM_PRIO", "OCG_HBM_PIPE", "HIP_VISIBLE_DEVICES")
+    return {k: os.environ.get(k) for k in keys}
 
 
 def st_traj_ms_per_step(eng, Nt):
@@ -538,12 +600,25 @@ def bench_c4(args):
     c = C5 if c5 else C4
     L, p, Q, dt = c["L"], c["p"], c["npart"], c["tstep"]
     eng = Engine(L, p, Q, c["J"], dt, c["cutoff"], c["maxm"], device=local, engine="hbm")
-    warm_s, cached = 0.0, bool(args.state_cache) and os.path.exists(args.state_cache)
-    if cached:   # prepared by an earlier (unprofiled) process
-        z = np.load(args.state_cache, allow_pickle=False)
-        ini = MPS(L, p, Q, z["ini_dims"], z["ini_data"])
-        tgt = MPS(L, p, Q, z["tgt_dims"], z["tgt_data"])
-    else:
+    # the state cache is keyed to what produced it; a file of another workload or
+    # preparation is ignored (and overwritten), never loaded silently
+    cache = args.state_cache
+    if cache and not cache.endswith(".npz"):
+        cache += ".npz"   # np.savez would append it
+    key = np.array([f"{args.workload[:2]} L={L} p={p} Q={Q} maxm={c['maxm']} dt={dt} "
+                    f"warm={args.c5_warm if c5 else 'c4_warm256'}"])
+    if cache and world > 1:
+        dist.barrier()    # rank 0 may still be writing it
+    warm_s, cached = 0.0, False
+    if cache and os.path.exists(cache):   # prepared by an earlier (unprofiled) process
+        z = np.load(cache, allow_pickle=False)
+        if "key" in z.files and str(z["key"][0]) == str(key[0]):
+            ini = MPS(L, p, Q, z["ini_dims"], z["ini_data"])
+            tgt = MPS(L, p, Q, z["tgt_dims"], z["tgt_data"])
+            cached = True
+        else:
+            print(f"[bench] state cache {cache} belongs to another preparation; preparing anew", file=sys.stderr)
+    if not cached:
         if c5:
             from optimalcontrolmps_amd.states import product_state, warm_state
             t0 = time.perf_counter()
@@ -553,8 +628,10 @@ def bench_c4(args):
             z = np.load(os.path.join(ROOT, "tests", "golden", "c4_warm256.npz"), allow_pickle=False)
             ini = MPS(L, p, Q, z["dims"], z["data"])
         tgt = eng.steps(ini, np.full(3, 6.0), True)
-        if args.state_cache and rank == 0:
-            np.savez(args.state_cache, ini_dims=ini.dims, ini_data=ini.data, tgt_dims=tgt.dims, tgt_data=tgt.data)
+        if cache and rank == 0:   # written whole, then renamed: a reader never sees a partial file
+            tmp = cache[:-4] + f".tmp{os.getpid()}.npz"
+            np.savez(tmp, key=key, ini_dims=ini.dims, ini_data=ini.data, tgt_dims=tgt.dims, tgt_data=tgt.data)
+            os.replace(tmp, cache)
     if args.prepare_only:
         if world > 1:
             dist.barrier()
@@ -674,8 +751,10 @@ def bench_c4(args):
                                        limiter="the per-sector Hermitian eigensolver (k_heev_*) sets the step time; "
                                                "k_gemm launches are small (tasks of m, n ~ 16-60) and latency-bound"),
         }
-        if world == 1 and not args.no_cpu_baseline and not c5 and not grad and not args.profiled:
-            res["cpu_baseline"] = cpu_baseline_c4(ini, tgt, Nt, args.cpu_threads)
+        res["env"] = run_env()
+        if world == 1 and not args.no_cpu_baseline and not grad and not args.profiled:
+            res["cpu_baseline"] = (cpu_baseline_c5(ini, Nt, args.cpu_threads) if c5 else
+                                   cpu_baseline_c4(ini, tgt, Nt, args.cpu_threads, args.c4_cpu_nt))
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
@@ -696,17 +775,24 @@ def measured_traffic(kernel, tag="r01"):
         return None
 
 
-def cpu_baseline_c4(ini, tgt, Nt, threads):
-    """Config 4 on the CPU restatement (oracle/, 'port'), a bounded sample: one
-    chi = 256 step of the bench's own chain (L=20, p=7, from psi_init at U 2.5 ->
-    3.0) on one host thread, with the oracle's Householder + QL block
-    eigensolver (ORC_HEEV=ql: LAPACK zheev's algorithm, as ITensor's
-    diagHermitian; the default cyclic Jacobi takes ~14x longer).  The getHessian
-    of this slice is then priced from that step: psi and xi (2 (N_t - 1) steps on
-    two threads, calcPsiXiDivT), xiH (N_t dH applications, ~2 steps each, over
-    the threads) and the rows' (N_t-2)(N_t-3)/2 steps over the threads, as the
-    reference's calcHessian_parallel schedules them; value = rows/s of that
-    estimate at the threads available (measured: the step)."""
+def cpu_baseline_c4(ini, tgt, Nt, threads, cpu_nt=5):
+    """Config 4 on the CPU restatement (oracle/, 'port', not ITensor), with the
+    oracle's Householder + QL block eigensolver (ORC_HEEV=ql: LAPACK zheev's
+    algorithm, as ITensor's diagHermitian; the default cyclic Jacobi takes ~14x
+    longer) on the same chain (psi_init, psi_target of the slice):
+      measured: one full getHessian at N_t = cpu_nt (default 5: 3 rows) on the
+        granted host threads — psi || xi on two threads, xiH and the rows over
+        the threads (src/OptimalControl.cpp:281-338), every thread budget also
+        splitting the U(1) sectors inside each step (bit-identical results) —
+        beside the GPU's getHessian of the same controls (same command, HIP),
+        with the two Hessians compared;
+      priced: the slice's own N_t from one measured chi = 256 step on one
+        thread (psi || xi serial, xiH (one dH application ~ 3 steps, measured at
+        8 threads: 17.9 s vs 6.0 s) and the rows' (N_t-2)(N_t-3)/2 steps over the
+        threads; overlaps not priced, so the estimate favours the CPU).
+    `value` is the measured rate (rows/s of the short N_t = cpu_nt getHessian,
+    whose rows average (cpu_nt - 3)/2 steps: it flatters the CPU next to the
+    slice's rows)."""
     os.environ["ORC_HEEV"] = "ql"   # read at the oracle's first decomposition in this process
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
@@ -714,6 +800,7 @@ def cpu_baseline_c4(ini, tgt, Nt, threads):
     L, p, Q = c["L"], c["p"], c["npart"]
     st = O.Stepper(L, p, Q, c["J"], c["tstep"], c["cutoff"], c["maxm"])
     psi0 = O.MPS(L, p, Q, ini.dims, ini.data)
+    O.set_sector_threads(1)
     t0 = time.perf_counter()
     st.step(psi0, 2.5, 3.0, True)
     t_step = time.perf_counter() - t0
@@ -721,14 +808,101 @@ def cpu_baseline_c4(ini, tgt, Nt, threads):
     th = max(1, min(threads, avail)) if threads else avail
     rows = Nt - 2
     row_steps = rows * (rows - 1) // 2
-    est = t_step * ((Nt - 1) + 2.0 * Nt / th + (row_steps + 2.0 * rows) / th)
+    est = t_step * ((Nt - 1) + 3.0 * Nt / th + (row_steps + 3.0 * rows) / th)
+    out = {"unit": "rows/s", "cores": th, "kind": "port", "host_threads_available": avail, "nproc": os.cpu_count(),
+           "priced_slice": {"value": rows / est, "unit": "rows/s", "estimated": True, "N_t": Nt, "threads": th,
+                            "measured_step_s_1thread": t_step,
+                            "sample": f"one chi=256 step of this chain on one thread ({t_step:.1f} s); the N_t={Nt} "
+                                      f"getHessian priced from it at {th} threads (psi || xi serial, dH = 3 steps, "
+                                      f"xiH and rows over the threads, overlaps not priced)"}}
+    if cpu_nt and cpu_nt >= 4:
+        u = np.random.default_rng(C4["seed"] + 99).uniform(2.0, 10.0, cpu_nt)
+        oc = O.OC(st, O.MPS(L, p, Q, tgt.dims, tgt.data), psi0, cpu_nt, 0.0)
+        oc.set_nested(True)
+        Hc = np.zeros((cpu_nt, cpu_nt))
+        t_h = oc.time_hessian(u, th, Hc)
+        out.update(value=(cpu_nt - 2) / t_h, measured_s=t_h, estimated=False,
+                   sample=f"one full getHessian at N_t={cpu_nt} ({cpu_nt - 2} rows) of this chain (psi_init, "
+                          f"psi_target of the slice, GRAPE controls U(2,10)) on the C++ CPU restatement (oracle/, not "
+                          f"ITensor; Householder + QL), {th} threads: psi || xi, xiH and rows over the threads, each "
+                          f"thread budget also splitting the U(1) sectors inside a step; {t_h:.1f} s")
+        out["gpu_same_sample"] = gpu_same_sample(u, tgt, ini, C4, Hc)
+    else:
+        out.update(value=out["priced_slice"]["value"], estimated=True, sample=out["priced_slice"]["sample"])
+    return out
+
+
+def gpu_same_sample(u, tgt, ini, c, Hc):
+    """the GPU's getHessian of the CPU sample's controls on the same chain (a
+    fresh HBM-engine context, one untimed warm-up call): rows/s and the largest
+    Hessian difference from the CPU restatement's, relative to max|H|"""
+    from optimalcontrolmps_amd.native import Engine
+    e = Engine(c["L"], c["p"], c["npart"], c["J"], c["tstep"], c["cutoff"], c["maxm"], engine="hbm")
+    e.set_states(tgt, ini)
+    e.hessian(u)
+    t0 = time.perf_counter()
+    H, _, _ = e.hessian(u)
+    t = time.perf_counter() - t0
+    e.close()
+    return {"value": (len(u) - 2) / t, "unit": "rows/s", "s": t,
+            "max_abs_diff_rel_to_max_H": float(np.abs(H - Hc).max() / max(np.abs(Hc).max(), 1e-300))}
+
+
+def step_cost_model(dims, L, p, Q):
+    """flop model of one BH_tDMRG step from the bond dims (flat (L+1)(Q+1)):
+    per gate and middle-bond sector q, Theta (8 R C m), Gram (8 n^2 N),
+    Householder + QL eigenproblem with vectors (~20 n^3) and the factors
+    (8 m R C), R / C the sector's row / column counts, n = min(R, C), N = max,
+    m = the sector's kept dim; the gauge moves scale the same way per gate"""
+    d = np.asarray(dims).reshape(L + 1, Q + 1)
+    tot = 0.0
+    for b in range(1, L):   # gate on sites (b, b+1): bonds b-1, b, b+1
+        for q in range(Q + 1):
+            R = sum(d[b - 1, q - n] for n in range(p) if 0 <= q - n <= Q)
+            C = sum(d[b + 1, q + n] for n in range(p) if q + n <= Q)
+            if R == 0 or C == 0:
+                continue
+            n, N, m = min(R, C), max(R, C), d[b, q]
+            tot += 16.0 * R * C * m + 8.0 * n * n * N + 20.0 * n ** 3
+    return tot
+
+
+def cpu_baseline_c5(ini, Nt, threads):
+    """Config 5 (L = 50, p = 9, chi = 512) on the CPU restatement, priced: one
+    chi = 512 step is measured on one thread on the 12-site chain of
+    tests/golden/c5_w512.npz (config 5's p and tstep, middle bonds saturated at
+    512 by the oracle itself; one L = 50 step would take minutes), scaled to the
+    L = 50 state by the flop model of both chains' bond dims (step_cost_model),
+    and the slice's getHessian is priced from that like config 4's (psi || xi
+    serial, dH = 3 steps, xiH and rows over the granted threads; overlaps not
+    priced)."""
+    os.environ["ORC_HEEV"] = "ql"
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    c = C5
+    z = np.load(os.path.join(ROOT, "tests", "golden", "c5_w512.npz"), allow_pickle=False)
+    Lx = 12
+    st = O.Stepper(Lx, c["p"], Lx, c["J"], c["tstep"], c["cutoff"], c["maxm"])
+    psi = O.MPS(Lx, c["p"], Lx, z["dims"], z["data"])
+    O.set_sector_threads(1)
+    t0 = time.perf_counter()
+    st.step(psi, 2.5, 3.0, True)
+    t12 = time.perf_counter() - t0
+    ratio = step_cost_model(ini.dims, c["L"], c["p"], c["npart"]) / step_cost_model(z["dims"], Lx, c["p"], Lx)
+    t50 = t12 * ratio
+    avail = cpu_threads_available()
+    th = max(1, min(threads, avail)) if threads else avail
+    rows = Nt - 2
+    row_steps = rows * (rows - 1) // 2
+    est = t50 * ((Nt - 1) + 3.0 * Nt / th + (row_steps + 3.0 * rows) / th)
     return {"value": rows / est, "unit": "rows/s", "cores": th, "kind": "port", "estimated": True,
-            "measured_step_s": t_step, "measured_sweep_steps_per_sec_1thread": 1.0 / t_step,
+            "measured_step_s_L12_1thread": t12, "model_ratio_L50_over_L12": ratio, "priced_step_s_L50": t50,
             "host_threads_available": avail, "nproc": os.cpu_count(),
-            "sample": f"one chi=256 step of this chain on the C++ CPU restatement (oracle/, not ITensor; Householder "
-                      f"+ QL block eigensolver) on one thread, {t_step:.1f} s; the N_t={Nt} getHessian priced from it "
-                      f"at {th} threads (psi || xi serial, xiH and rows over the threads; the overlaps are not priced, "
-                      f"so the estimate favours the CPU)"}
+            "sample": f"one chi=512 step of the 12-site config-5 chain (tests/golden/c5_w512.npz) on the C++ CPU "
+                      f"restatement (oracle/, not ITensor; Householder + QL) on one thread, {t12:.1f} s, scaled "
+                      f"x{ratio:.1f} to the L=50 state by a flop model of the bond dims; the N_t={Nt} getHessian "
+                      f"priced from it at {th} threads (psi || xi serial, dH = 3 steps, xiH and rows over the threads, "
+                      f"overlaps not priced, so the estimate favours the CPU)"}
 
 
 def cpu_threads_available():

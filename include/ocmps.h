@@ -35,6 +35,7 @@ extern "C" {
 #define OCG_EHIP 3      /* HIP runtime error (no GPU, launch failure, ...) */
 #define OCG_ESTATE 4    /* call order violated (e.g. rows before trajectories) */
 #define OCG_ENUM 5      /* numerical failure flagged by a kernel */
+#define OCG_ENOMEM 6    /* device or pinned host allocation failed (HBM engine) */
 
 typedef struct ocg_ctx ocg_ctx;
 
@@ -215,7 +216,11 @@ int ocg_denmat_decomp(ocg_ctx* ctx, int nm, const int* rows, const int* cols, co
  * 2 dH apply, 3 Hessian rows, 4 steps, 5 fused pipeline (ocg_hessian phase 1),
  * 6 batched row overlaps (ocg_hessian phase 2), 7 the HBM engine's MFMA GEMM
  * kernel (k_gemm: HIP-event time, algorithmic bytes and flops of its tasks;
- * zeros on the LDS engine).  Sums since the last reset. */
+ * zeros on the LDS engine), 8 the HBM engine's getHessian path counters
+ * (*launches = pipelined getHessians completed, *sweep_steps = two-phase
+ * retries after a pipeline that failed with OCG_ENOMEM; never with
+ * OCG_HBM_PIPE=1, which makes any pipeline failure the call's status).  Sums
+ * since the last reset. */
 int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
                      double* alg_flops, long* sweep_steps);
 int ocg_reset_stats(ocg_ctx* ctx);

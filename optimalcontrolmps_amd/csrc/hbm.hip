@@ -49,6 +49,14 @@ struct Error : std::runtime_error {
     hipError_t e_ = (expr);                                                                       \
     if (e_ != hipSuccess) throw ::hbm::Error(3, std::string(#expr) + ": " + hipGetErrorString(e_));     \
   } while (0)
+// allocations: out of device / pinned memory is its own status (OCG_ENOMEM), the
+// only failure after which ocg_hessian may retry a getHessian on another path
+#define HCKA(expr)                                                                                \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess)                                                                         \
+      throw ::hbm::Error(e_ == hipErrorOutOfMemory ? 6 : 3, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
 
 constexpr double kGaugeCutoff = 1e-14;  // = OCG_GAUGE_CUTOFF of the LDS engine and the oracle
 constexpr int kNoMaxm = 1 << 30;
@@ -112,7 +120,7 @@ struct DBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    HCK(hipMalloc(&p, sizeof(T) * n));
+    HCKA(hipMalloc(&p, sizeof(T) * n));
     cap = n;
   }
   ~DBuf() {
@@ -430,6 +438,20 @@ struct Engine {
     for (size_t i = 0; i < vec.size(); ++i)
       if (vec[i].get() == c) { (c->wide ? free_chain_w : free_chain).push_back(int(i)); return; }
   }
+  // Give the pool back down to n chains (every chain must be free): after a failed
+  // call that grew it, so that the path the caller retries sees that memory free.
+  void shrink_chains(int n) {
+    if (n >= nchain_cap) return;
+    if (int(free_chain.size()) != nchain_cap) throw Error(4, "internal: chain pool shrunk while chains are in use");
+    sync();
+    if (chain_pool.p) (void)hipFree(chain_pool.p);
+    chain_pool.p = nullptr;
+    chain_pool.cap = 0;
+    chains.clear();
+    free_chain.clear();
+    nchain_cap = 0;
+    if (n > 0) reserve_chains(n, false);
+  }
   // Chains are held only inside one entry point: after a failed call every
   // chain is free again (the error path of guard()).
   void release_all() {
@@ -503,11 +525,11 @@ struct Engine {
         char* ptr = nullptr;
         if (pinned) {
           // coherent (not cached by the device): small task lists are read in place
-          HCK(hipHostMalloc((void**)&ptr, sz, hipHostMallocCoherent));
+          HCKA(hipHostMalloc((void**)&ptr, sz, hipHostMallocCoherent));
           void* dp = nullptr;
           if (hipHostGetDevicePointer(&dp, ptr, 0) != hipSuccess || dp != ptr) same_va = false;
         }
-        else HCK(hipMalloc((void**)&ptr, sz));
+        else HCKA(hipMalloc((void**)&ptr, sz));
         blk.push_back({ptr, sz});
         top = 0;
       }
@@ -2200,6 +2222,9 @@ int guard(hbm_engine* h, F f) {
   } catch (const hbm::Error& e) {
     h->err = e.what();
     rc = e.code;
+  } catch (const std::bad_alloc& e) {
+    h->err = std::string("host allocation failed: ") + e.what();
+    rc = 6;
   } catch (const std::exception& e) {
     h->err = e.what();
     rc = 3;
@@ -2481,10 +2506,12 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
     // afterwards, on success and on failure, down to the heap the call began with
     // (a previous pipelined getHessian's row-state slots stay for its next call)
     const size_t keep = std::max(size_t(extra0), E.heap_slots);
-    struct Shrink {
+    struct ShrinkOnError {  // unwinding only: the success path shrinks inside the guard
       hbm::Engine& E;
       size_t keep;
-      ~Shrink() {
+      bool ok = false;
+      ~ShrinkOnError() {
+        if (ok) return;
         try {
           E.drain();
           E.shrink_states(keep);
@@ -2535,6 +2562,8 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
     for (int k = 0; k < K; ++k) fx[k] = pb(k) + N - 1;
     auto rf = hbm_pairs(h, fx, fy, false);
     for (int k = 0; k < K; ++k) { F[2 * k] = rf[k].real(); F[2 * k + 1] = rf[k].imag(); }
+    shrink.ok = true;
+    E.shrink_states(keep);  // a device failure here is this call's status
   });
 }
 
@@ -3028,21 +3057,32 @@ int hbm_hessian_pipe(hbm_engine* h, const double* u, int N, const int* rows, int
     std::vector<int> rsoff(nrows + 1);
     rsoff[0] = psih0 + N;
     for (int k = 0; k < nrows; ++k) rsoff[k + 1] = rsoff[k] + (N - 2 - rs[k]);
-    // a failed call gives its row-state slots back (the caller then runs the
-    // two-phase path, which must see that memory free)
+    // a failed call gives back everything it grew — its row-state slots, the
+    // context engine's chain pool, the two worker engines with their pools and
+    // arenas — so that the two-phase path ocg_hessian may retry after an
+    // allocation failure sees that memory free
     struct ShrinkOnError {
-      hbm::Engine& E;
+      hbm_engine* h;
       size_t keep;
+      int chains0;
       bool ok = false;
       ~ShrinkOnError() {
         if (ok) return;
+        hbm::Engine& E = *h->E;
         try {
           E.drain();
+          for (auto& W : h->W)
+            if (W) {
+              W->drain();
+              W.reset();
+            }
+          E.release_all();
+          E.shrink_chains(chains0);
           E.shrink_states(keep);
         } catch (...) {
         }
       }
-    } undo{E, std::max(E.heap_slots, size_t(h->xih_base() + N + 2))};
+    } undo{h, std::max(E.heap_slots, size_t(h->xih_base() + N + 2)), E.nchain_cap};
     E.reserve_states(size_t(rsoff[nrows]));
     hbm::Engine& WH = pipe_worker(h, 0);
     hbm::Engine& WX = pipe_worker(h, 1);

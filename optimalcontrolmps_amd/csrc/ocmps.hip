@@ -196,6 +196,9 @@ struct ocg_ctx {
   double J = 1.0;
   std::vector<int> md;  // (L+1)*Q1 rank bounds
   std::string err;
+  // HBM engine getHessian path counters (ocg_kernel_stats kind 8): pipelined
+  // calls completed, and two-phase retries after a pipeline that ran out of memory
+  long pipe_runs = 0, pipe_fallbacks = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};  // ocg_hessian phase marks
@@ -1279,16 +1282,25 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     if (pipe_env != 0 && !reuse && nrows > 0) {
       size_t fr = 0, tot = 0;
       HIPCHK(c, hipMemGetInfo(&fr, &tot));
-      if (hbm_pipe_bytes(c->hbm, N, rows, nrows) <= 0.5 * double(fr)) {
+      if (pipe_env == 1 || hbm_pipe_bytes(c->hbm, N, rows, nrows) <= 0.5 * double(fr)) {
         c->u_psi.clear();
         c->u_xi.clear();
-        if (hb(c, hbm_hessian_pipe(c->hbm, u, N, rows, nrows, H, divT, F)) == 0) {
+        const int rc = hb(c, hbm_hessian_pipe(c->hbm, u, N, rows, nrows, H, divT, F));
+        if (rc == 0) {
+          ++c->pipe_runs;
           note_u(c, u, N, 3);
           return 0;
         }
-        // a pipeline that still fails (allocation of a worker's pools or arenas)
-        // has given its row-state slots back: the two-phase path runs instead and
-        // writes the same entries of H
+        // Only a pipeline that ran out of memory (a worker's pools or arenas
+        // beyond the estimate) is retried, and only when the pipeline was not
+        // asked for explicitly: it has given back everything it grew, and the
+        // two-phase path writes the same entries of H.  Any other failure is the
+        // call's status.
+        if (rc != OCG_ENOMEM || pipe_env == 1) return rc;
+        ++c->pipe_fallbacks;
+        const int rc2 = hessian_unfused(c, u, N, rows, nrows, H, divT, F);
+        if (rc2 == 0) c->err.clear();
+        return rc2;
       }
     }
     return hessian_unfused(c, u, N, rows, nrows, H, divT, F);
@@ -1571,7 +1583,15 @@ int ocg_get_state(ocg_ctx* c, int which, int t, int* dims, double* data, size_t 
 
 int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, double* alg_bytes, double* alg_flops,
                      long* sweep_steps) {
-  if (!c || kind < 0 || kind > 7) return OCG_EINVAL;
+  if (!c || kind < 0 || kind > 8) return OCG_EINVAL;
+  if (kind == 8) {  // getHessian path counters (HBM engine; zeros on the LDS engine)
+    if (total_ms) *total_ms = 0;
+    if (launches) *launches = c->pipe_runs;
+    if (alg_bytes) *alg_bytes = 0;
+    if (alg_flops) *alg_flops = 0;
+    if (sweep_steps) *sweep_steps = c->pipe_fallbacks;
+    return 0;
+  }
   if (c->hbm) return hb(c, hbm_stats(c->hbm, kind, total_ms, launches, alg_bytes, alg_flops, sweep_steps));
   if (kind == 7) {  // the MFMA contraction kernel exists only in the HBM engine
     if (total_ms) *total_ms = 0;
@@ -1612,6 +1632,7 @@ int ocg_profile(ocg_ctx* c, double* out32, int reset) {
 
 int ocg_reset_stats(ocg_ctx* c) {
   if (!c) return OCG_EINVAL;
+  c->pipe_runs = c->pipe_fallbacks = 0;
   if (c->hbm) {
     hbm_reset_stats(c->hbm);
     return 0;

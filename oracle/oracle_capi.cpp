@@ -120,6 +120,10 @@ void* orc_oc_new(void* h, const int* fdt, const double* dt_, const int* fdi, con
   return o;
 }
 void orc_oc_free(void* o) { delete static_cast<OrcOC*>(o); }
+// nested != 0: getHessian's threads also split the U(1) sectors inside each step
+void orc_oc_set_nested(void* o, int nested) { static_cast<OrcOC*>(o)->oc->nested = nested; }
+// sector threads of the calling thread's steps / applications (1: serial)
+void orc_set_sector_threads(int n) { sector_threads() = n < 1 ? 1 : n; }
 void orc_oc_set_gamma(void* o, double g) { static_cast<OrcOC*>(o)->oc->gamma = g; }
 
 double orc_oc_cost(void* o, const double* u) {

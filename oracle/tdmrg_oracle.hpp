@@ -42,6 +42,46 @@ namespace oracle {
 using cplx = std::complex<double>;
 
 // ---------------------------------------------------------------------------
+// Sector parallelism (CPU-baseline speed only).  The U(1) blocks of one
+// decomposition / Theta build / gauge move are independent: with a budget of
+// T > 1 threads on the calling thread they are dealt over T threads, largest
+// first.  Every block is computed by one thread with the same loops, so the
+// results are bit-identical to T = 1 (tests/test_oracle.py).  The budget is per
+// thread (default 1, or ORC_SECTOR_THREADS); workers run with a budget of 1.
+// ---------------------------------------------------------------------------
+inline int& sector_threads() {
+  static thread_local int t = [] {
+    const char* e = std::getenv("ORC_SECTOR_THREADS");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  return t;
+}
+// f(q) for every q in [0, n) with cost[q] > 0, largest cost first
+template <class F>
+inline void par_sectors(int n, const std::vector<double>& cost, F f) {
+  std::vector<int> order;
+  for (int q = 0; q < n; ++q)
+    if (cost[q] > 0) order.push_back(q);
+  const int T = std::min<int>(sector_threads(), int(order.size()));
+  if (T <= 1) {
+    for (int q : order) f(q);
+    return;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+  std::atomic<size_t> next(0);
+  auto work = [&]() {
+    sector_threads() = 1;
+    for (size_t i; (i = next.fetch_add(1)) < order.size();) f(order[i]);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(work);
+  const int mine = sector_threads();
+  work();
+  sector_threads() = mine;
+  for (auto& th : pool) th.join();
+}
+
+// ---------------------------------------------------------------------------
 // Dense helpers
 // ---------------------------------------------------------------------------
 struct Blk {
@@ -385,9 +425,15 @@ inline Decomp decompose(const QMat& M, Dir dir, double cutoff, int maxm) {
   std::vector<std::vector<cplx>> V(Q + 1);
   struct Ev { double lam; int q, i; };
   std::vector<Ev> all;
+  std::vector<double> cost(Q + 1, 0.0);
   for (int q = 0; q <= Q; ++q) {
     const Blk& B = M.blk[q];
     if (B.empty()) continue;
+    const double n = (dir == Fromleft) ? B.r : B.c;
+    cost[q] = n * n * (n + double(B.r) * B.c / n);
+  }
+  par_sectors(Q + 1, cost, [&](int q) {
+    const Blk& B = M.blk[q];
     int n = (dir == Fromleft) ? B.r : B.c;
     std::vector<cplx> rho(size_t(n) * n, cplx(0, 0));
     if (dir == Fromleft) {
@@ -406,8 +452,9 @@ inline Decomp decompose(const QMat& M, Dir dir, double cutoff, int maxm) {
         }
     }
     heev(n, rho, w[q], V[q]);
-    for (int i = 0; i < n; ++i) all.push_back({w[q][i], q, i});
-  }
+  });
+  for (int q = 0; q <= Q; ++q)
+    for (int i = 0; i < int(w[q].size()); ++i) all.push_back({w[q][i], q, i});
   std::stable_sort(all.begin(), all.end(), [](const Ev& a, const Ev& b) {
     if (a.lam != b.lam) return a.lam > b.lam;
     if (a.q != b.q) return a.q < b.q;
@@ -421,9 +468,10 @@ inline Decomp decompose(const QMat& M, Dir dir, double cutoff, int maxm) {
   for (int j = 0; j < m; ++j) D.kept[all[j].q]++;  // per block the top-k (block-sorted)
   D.X.assign(Q + 1, Blk());
   D.Y.assign(Q + 1, Blk());
-  for (int q = 0; q <= Q; ++q) {
+  std::vector<double> fcost(Q + 1, 0.0);
+  for (int q = 0; q <= Q; ++q) fcost[q] = double(D.kept[q]) * M.blk[q].r * M.blk[q].c;
+  par_sectors(Q + 1, fcost, [&](int q) {
     int k = D.kept[q];
-    if (k == 0) continue;
     const Blk& B = M.blk[q];
     if (dir == Fromleft) {
       int n = B.r;
@@ -450,7 +498,7 @@ inline Decomp decompose(const QMat& M, Dir dir, double cutoff, int maxm) {
         }
       D.X[q] = std::move(X); D.Y[q] = std::move(Y);
     }
-  }
+  });
   return D;
 }
 
@@ -527,7 +575,9 @@ inline void gauge_right(MPS& m, int k) {
   }
   // A_{k+1} <- Y * A_{k+1}
   std::vector<Blk> nb(size_t(m.Q + 1) * m.p);
-  for (int q = 0; q <= m.Q; ++q)
+  std::vector<double> cost(m.Q + 1, 0.0);
+  for (int q = 0; q <= m.Q; ++q) cost[q] = double(D.kept[q]) * m.d(k, q) * (m.d(k + 1, q) + 1);
+  par_sectors(m.Q + 1, cost, [&](int q) {
     for (int n = 0; n < m.p && q + n <= m.Q; ++n) {
       const Blk& S = m.blk(k + 1, q, n);
       int kq = D.kept[q];
@@ -541,6 +591,7 @@ inline void gauge_right(MPS& m, int k) {
         }
       nb[size_t(q) * m.p + n] = std::move(T);
     }
+  });
   (void)old;
   m.A[k] = std::move(nb);  // site k+1
 }
@@ -561,7 +612,9 @@ inline void gauge_left(MPS& m, int k) {
   }
   // A_{k-1} <- A_{k-1} * X
   std::vector<Blk> nb(size_t(m.Q + 1) * m.p);
-  for (int ql = 0; ql <= m.Q; ++ql)
+  std::vector<double> cost(m.Q + 1, 0.0);
+  for (int ql = 0; ql <= m.Q; ++ql) cost[ql] = double(m.d(k - 2, ql) + 1) * m.p * 64.0;
+  par_sectors(m.Q + 1, cost, [&](int ql) {
     for (int n = 0; n < m.p && ql + n <= m.Q; ++n) {
       const Blk& S = m.blk(k - 1, ql, n);
       int q = ql + n, kq = D.kept[q];
@@ -575,6 +628,7 @@ inline void gauge_left(MPS& m, int k) {
         }
       nb[size_t(ql) * m.p + n] = std::move(T);
     }
+  });
   m.A[k - 2] = std::move(nb);
 }
 
@@ -725,11 +779,17 @@ struct Stepper {
     T.blk.assign(Q + 1, Blk());
     T.rowoff.assign(Q + 1, std::vector<int>(p, -1));
     T.coloff.assign(Q + 1, std::vector<int>(p, -1));
+    std::vector<double> cost(Q + 1, 0.0);
     for (int q = 0; q <= Q; ++q) {
       int R = 0, C = 0;
       for (int n1 = 0; n1 < p; ++n1) if (m.d(l, q - n1) > 0) { T.rowoff[q][n1] = R; R += m.d(l, q - n1); }
       for (int n2 = 0; n2 < p; ++n2) if (q + n2 <= Q && m.d(r, q + n2) > 0) { T.coloff[q][n2] = C; C += m.d(r, q + n2); }
-      if (R == 0 || C == 0) continue;
+      if (R > 0 && C > 0) cost[q] = double(R) * C * (m.d(mid, q) + 1);
+    }
+    par_sectors(Q + 1, cost, [&](int q) {
+      int R = 0, C = 0;
+      for (int n1 = 0; n1 < p; ++n1) if (T.rowoff[q][n1] >= 0) R += m.d(l, q - n1);
+      for (int n2 = 0; n2 < p; ++n2) if (T.coloff[q][n2] >= 0) C += m.d(r, q + n2);
       Blk B(R, C);
       if (m.d(mid, q) > 0) {
         for (int n1 = 0; n1 < p; ++n1) {
@@ -748,7 +808,7 @@ struct Stepper {
         }
       }
       T.blk[q] = std::move(B);
-    }
+    });
     return T;
   }
 
@@ -757,8 +817,11 @@ struct Stepper {
                   const std::vector<cplx>& pre1, const std::vector<cplx>& pre2,
                   const std::vector<cplx>& post1, const std::vector<cplx>& post2) const {
     int l = i1 - 1, r = i1 + 1;
-    std::vector<cplx> v(p), w(p);
+    std::vector<double> cost(Q + 1, 0.0);
     for (int ql = 0; ql <= Q; ++ql)
+      for (int qr = ql; qr <= Q; ++qr) cost[ql] += double(m.d(l, ql)) * m.d(r, qr);
+    par_sectors(Q + 1, cost, [&](int ql) {
+      std::vector<cplx> v(p), w(p);
       for (int ia = 0; ia < m.d(l, ql); ++ia)
         for (int qr = ql; qr <= Q; ++qr)
           for (int ic = 0; ic < m.d(r, qr); ++ic) {
@@ -780,6 +843,7 @@ struct Stepper {
               T.blk[q].at(T.rowoff[q][n1] + ia, T.coloff[q][n2] + ic) = w[n1];
             }
           }
+    });
   }
 
   // write a decomposition of Θ back into sites i1, i2 (new middle bond)
@@ -916,7 +980,9 @@ struct Stepper {
         }
       }
       std::vector<Blk> nb(size_t(Q + 1) * p);
-      for (int ql = 0; ql <= Q; ++ql)
+      std::vector<double> cost(Q + 1, 0.0);
+      for (int ql = 0; ql <= Q; ++ql) cost[ql] = double(phi.d(k - 2, ql) + 1) * p * 64.0;
+      par_sectors(Q + 1, cost, [&](int ql) {
         for (int n = 0; n < p && ql + n <= Q; ++n) {
           const Blk& S = phi.blk(k - 1, ql, n);
           int q = ql + n, kq = D.kept[q];
@@ -930,6 +996,7 @@ struct Stepper {
             }
           nb[size_t(ql) * p + n] = std::move(T);
         }
+      });
       phi.A[k - 2] = std::move(nb);
     }
     return phi;
@@ -1034,10 +1101,18 @@ struct OC {
   // threads > 1: psi and xi on two threads (calcPsiXiDivT, :424-430) and the
   // xiH list by the worker pool (the reference builds it serially, :300-303;
   // every entry is computed independently, so the result is the same).
+  // nested != 0 (CPU baseline of the large configs): the threads also serve the
+  // sector parallelism inside each step — psi and xi get threads / 2 each, the
+  // row workers threads / workers each (same numbers bit for bit).
+  int nested = 0;
   std::vector<double> hessian(const std::vector<double>& u, int threads) {
+    const int outer = sector_threads();
     if (threads > 1) {
-      std::thread tx([&]() { calcXi(u); });
+      const int half = nested ? std::max(1, threads / 2) : 1;
+      std::thread tx([&]() { sector_threads() = half; calcXi(u); });
+      sector_threads() = half;
       calcPsi(u);
+      sector_threads() = outer;
       tx.join();
     } else {
       calcPsi(u);
@@ -1053,8 +1128,11 @@ struct OC {
     if (threads > 1) {
       std::atomic<size_t> next(0);
       std::vector<std::thread> pool;
-      for (int t = 0; t < threads; ++t)
+      const int workers = nested ? std::min<int>(threads, int(N)) : threads;
+      const int per = nested ? std::max(1, threads / std::max(1, workers)) : 1;
+      for (int t = 0; t < workers; ++t)
         pool.emplace_back([&]() {
+          sector_threads() = per;
           for (size_t i; (i = next.fetch_add(1)) < N;) xiH[i] = st.apply_dH(xi_t[i]);
         });
       for (auto& th : pool) th.join();
@@ -1072,8 +1150,11 @@ struct OC {
     // worker pool with a shared row counter (:306-335); rows write disjoint entries
     std::atomic<size_t> next(1);
     std::vector<std::thread> pool;
-    for (int t = 0; t < threads; ++t)
+    const int workers = nested ? std::min<int>(threads, int(N) - 2) : threads;
+    const int per = nested ? std::max(1, threads / std::max(1, workers)) : 1;
+    for (int t = 0; t < workers; ++t)
       pool.emplace_back([&]() {
+        sector_threads() = per;
         for (;;) {
           size_t i = next.fetch_add(1);
           if (i + 1 >= N) break;

@@ -57,6 +57,8 @@ def lib():
         L.orc_oc_hessian.argtypes = [C.c_void_p, dp, C.c_int, dp]
         L.orc_oc_rows.argtypes = [C.c_void_p, dp, ip, C.c_int, dp]
         L.orc_oc_state.argtypes = [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.orc_oc_set_nested.argtypes = [C.c_void_p, C.c_int]
+        L.orc_set_sector_threads.argtypes = [C.c_int]
         L.orc_oc_time_hessian.restype = C.c_double
         L.orc_oc_time_hessian.argtypes = [C.c_void_p, dp, C.c_int, dp]
         _lib = L
@@ -212,8 +214,17 @@ class OC:
         assert rc == 0, rc
         return out.reshape(self.N, self.N)
 
-    def time_hessian(self, u, threads=1):
+    def set_nested(self, on=True):
+        """getHessian's threads also split the U(1) sectors inside each step (CPU
+        baseline of the large configs; the same numbers bit for bit)"""
+        lib().orc_oc_set_nested(self.h, int(on))
+
+    def time_hessian(self, u, threads=1, out=None):
+        """wall seconds of one getHessian; its Hessian into out (N x N float64) if given"""
         uu, pu = _d(u)
+        if out is not None:
+            assert out.dtype == np.float64 and out.flags.c_contiguous and out.size == self.N * self.N
+            return lib().orc_oc_time_hessian(self.h, pu, threads, out.ctypes.data_as(dp))
         return lib().orc_oc_time_hessian(self.h, pu, threads, None)
 
     def state(self, which, t):
@@ -222,6 +233,11 @@ class OC:
                                 self.st.cap, C.byref(n))
         assert rc == 0, rc
         return self.st._wrap(fd, d, n)
+
+
+def set_sector_threads(n):
+    """U(1)-sector threads of this (calling) thread's oracle steps (1: serial)"""
+    lib().orc_set_sector_threads(int(n))
 
 
 def heev(A):

@@ -69,9 +69,36 @@ def test_main_spawns_without_launcher(monkeypatch):
     calls = []
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(bench, "spawn_ranks", lambda n, argv: calls.append(("spawn", n)) or 0)
-    monkeypatch.setattr(bench, "run", lambda args: calls.append(("run", args.gpus)) or 0)
+    monkeypatch.setattr(bench, "run", lambda args, blocks=None: calls.append(("run", args.gpus, blocks)) or 0)
+    monkeypatch.setattr(bench, "slice_blocks", lambda args: {"config4_slice": {}, "config5_slice": {}})
     assert bench.main(["--gpus", "4"]) == 0
     monkeypatch.setenv("WORLD_SIZE", "4")
     assert bench.main(["--gpus", "4"]) == 0
     assert bench.main(["--gpus", "1"]) == 0
-    assert calls == [("spawn", 4), ("run", 4), ("run", 1)]
+    monkeypatch.delenv("WORLD_SIZE")
+    assert bench.main(["--gpus", "1"]) == 0                    # N=1 default: the slice blocks first
+    assert bench.main(["--gpus", "1", "--no-slices"]) == 0
+    assert bench.main(["--gpus", "1", "--profiled"]) == 0
+    assert calls == [("spawn", 4), ("run", 4, None), ("run", 1, None),
+                     ("run", 1, {"config4_slice": {}, "config5_slice": {}}), ("run", 1, None), ("run", 1, None)]
+
+
+def test_slice_blocks_children(monkeypatch):
+    """the config-4 / config-5 blocks run as fresh `bench.py --workload ...`
+    interpreters without the rank environment; a failing child leaves an
+    `error` field and the other block intact"""
+    import subprocess
+    seen = []
+
+    def fake_run(cmd, **kw):
+        seen.append((cmd, kw["env"]))
+        if "c4rows" in cmd:
+            return subprocess.CompletedProcess(cmd, 0, stdout='[x] noise\n{"metric": "c4", "value": 1.0}\n')
+        return subprocess.CompletedProcess(cmd, 1, stdout="Traceback ...\n")
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setenv("RANK", "0")
+    out = bench.slice_blocks(bench.parse_args(["--gpus", "1"]))
+    assert out["config4_slice"]["value"] == 1.0 and "error" not in out["config4_slice"]
+    assert "error" in out["config5_slice"] and "child_wall_s" in out["config5_slice"]
+    assert [c[0][3:5] for c in seen] == [["--workload", "c4rows"], ["--workload", "c5rows"]]
+    assert all("RANK" not in env for _, env in seen)

@@ -157,6 +157,7 @@ def test_c5_w512_pipelined_equals_stored(warm512, monkeypatch):
         eng = _engine(monkeypatch, OCG_HBM_PIPE=mode)
         eng.set_states(tgt, ini)
         out[mode] = eng.hessian(u)
+        assert eng.stats(8)["launches"] == (1 if mode == "1" else 0) and eng.stats(8)["sweep_steps"] == 0
         eng.close()
     (H0, d0, F0), (H1, d1, F1) = out["0"], out["1"]
     assert np.array_equal(H0, H1) and np.array_equal(d0, d1) and F0 == F1
@@ -230,6 +231,7 @@ def test_c5_w512_L12_hessian_vs_oracle(monkeypatch, pipe):
     eng = Engine(Lx, p, Nx, J, DT, CUT, MAXM, engine="hbm")
     eng.set_states(psi, psi)
     H, divT, F = eng.hessian(z["u"])
+    assert eng.stats(8)["launches"] == (1 if pipe == "1" else 0) and eng.stats(8)["sweep_steps"] == 0
     g = DT * (divT * F * 1j).real
     Fo = complex(z["F"][0])
     assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12

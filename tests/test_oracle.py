@@ -172,3 +172,31 @@ def test_heev_ql_vs_numpy_and_jacobi(n):
     assert np.abs(w - wj).max() <= 1e-14 * scale * max(1, n / 16)
     assert np.abs(V.conj().T @ V - np.eye(n)).max() <= 1e-13
     assert np.abs(A @ V - V * w).max() <= 1e-14 * scale * max(1, n / 16)
+
+
+def test_sector_parallel_oracle_bitwise(states, oracle_golden):
+    """The sector-parallel oracle (ORC_SECTOR_THREADS / the nested getHessian the
+    large configs' CPU baselines use) computes every U(1) block with the same
+    loops on one thread, so its Hessian, gradient and states equal the serial
+    oracle's bit for bit."""
+    name, (L, p, N, J), Ui, Uf, dt, cut, maxm = CASES[1]
+    u = oracle_golden[name + "/u"]
+
+    def make():
+        return O.OC(O.Stepper(L, p, N, J, dt, cut, maxm or 5000), orc_state(states, L, p, N, J, Uf),
+                    orc_state(states, L, p, N, J, Ui), len(u), 0.0)
+    ref = make()
+    H0 = ref.hessian(u, 1)
+    par = make()
+    par.set_nested(True)
+    H1 = par.hessian(u, 6)
+    assert np.array_equal(H0, H1)
+    st = O.Stepper(L, p, N, J, dt, cut, maxm or 5000)
+    psi = orc_state(states, L, p, N, J, Ui)
+    a = st.steps(psi, u[:6])
+    O.set_sector_threads(4)
+    try:
+        b = st.steps(psi, u[:6])
+    finally:
+        O.set_sector_threads(1)
+    assert np.array_equal(a.dims, b.dims) and np.array_equal(a.data, b.data)
