@@ -46,6 +46,7 @@ typedef struct ocg_info {
   int lds_bytes;          /* dynamic LDS of one chain workgroup */
   int block_threads;      /* threads per chain workgroup */
   int device;
+  int fast_chain;         /* 1: every step runs on the one-wave padded chain (LDS engine, small bonds) */
 } ocg_info;
 
 /* --------------------------------------------------------------- context

@@ -42,6 +42,9 @@ struct OcgParams {
   int imag;                 // 1: imaginary-time steps exp(-dt H) (ground-state preparation), 0: exp(-i dt H)
   int* err;                 // device error word of the context (bit 0: Jacobi sweep cap
                             // reached, bit 1: pipeline watchdog); checked after every launch
+  const int* fplan;         // plan image of the one-wave padded chain (fast_chain.hpp), or null:
+                            // every step of the kernels that step runs on it
+  int fast_off;             // byte offset of its region in the dynamic LDS
 };
 #define OCG_ERR_JACOBI 1
 #define OCG_ERR_WATCHDOG 2

@@ -1,0 +1,690 @@
+// MI355X (gfx950) one-wave padded chain: BH_tDMRG::step for chains whose
+// bond sectors all stay small (config 1: L=5, p=5, Npart=5, bonds <= 14).
+//
+// The generic chain (engine_device.hpp) rebuilds its block tables from the
+// runtime bond dimensions and runs every phase on two waves separated by
+// workgroup barriers; at config 1 a step costs ~165 k cycles there, most of
+// it bookkeeping and barrier / LDS round trips around tiny blocks.  Here every
+// bond sector is stored at its Schmidt-rank bound, zero-padded (fast_plan.hpp),
+// so the layout of every site, Θ, matricisation and factor is fixed and the
+// whole step is a replay of host-built descriptor tables by ONE wave: no
+// workgroup barrier, no table scan, a wave-level fence between phases.  Every
+// phase is written for instruction-level parallelism: a lane's descriptors for
+// all its elements are loaded at once, then all their operands (inner loops
+// unrolled to the compile-time bounds of fast.hpp with clamped addresses and
+// selects), so a phase costs two or three LDS round trips instead of one per
+// loop iteration.
+//
+// The arithmetic is that of Chain::step (reference src/BH_tDMRG.cpp:111-230
+// with ITensor denmatDecomp / position): Θ = A_i1 A_i2, pre-phase -> hopping
+// gate -> post-phase, per-sector Gram on the smaller side, register Jacobi
+// (16-lane groups, DPP partner exchange), the ITensor truncation rule
+// (relative cutoff, Maxm, floor 1e-30, rank bound), factors, gauge moves with
+// the 1e-14 gauge cutoff, closing phase and normalisation.  Padded rows /
+// columns are exact zeros, their Gram eigenvalues are exact zeros and are
+// always discarded, so results agree with the generic chain to rounding
+// (tests/test_fast_chain.py, tests/test_emu.py).
+//
+// Only wave 0 of the workgroup works; the other waves skip every call, and no
+// call contains a workgroup barrier.
+#pragma once
+
+#include "engine_device.hpp"
+#include "fast.hpp"
+
+namespace ocg {
+
+struct FastChain {
+  using CH = Chain<64>;  // its static Jacobi helpers (rotation, DPP partners, bpermute)
+  const OcgParams& P;
+  const int lane;
+  const bool act;  // wave 0
+  lzp MP, TH, TG, WB, XS, GT, PH;
+  LDS double *LAM, *SIG;
+  LDS int *DIM, *BOF, *KQ, *WIDX, *PL;
+  int np, nblk, o_blk, o_ls, o_site, o_siten, nops, centre_open;
+  double ph_u = __builtin_nan("");
+  int ph_dir = -1;
+  // dims_epoch counts bond-dimension changes (block offsets are recomputed
+  // only after one)
+  int dims_epoch = 0, bof_epoch = -1;
+  // algorithmic-traffic model (the general chain's accounting), per lane
+  double m_bytes = 0, m_flops = 0;
+  // diagnostic build (-DOCG_PROFILE): shader-clock cycles per phase into the
+  // general chain's PROF slots (the same categories as Chain::pf)
+  LDS double* PROF = nullptr;
+  unsigned long long pf_last = 0;
+  int pf_cur = 0;
+  __device__ __forceinline__ void pf(int cat) {
+#ifdef OCG_PROFILE
+    if (threadIdx.x == 0 && PROF) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (pf_last) PROF[pf_cur] += double(t - pf_last);
+      pf_last = t;
+      pf_cur = cat;
+    }
+#else
+    (void)cat;
+#endif
+  }
+
+  // base: the fast region of the dynamic LDS (fast_lds_bytes of the plan)
+  __device__ OCG_INLINE FastChain(const OcgParams& P_, char* base, const int* gplan, LDS double* prof = nullptr)
+      : P(P_), lane(threadIdx.x & 63), act(threadIdx.x < 64), PROF(prof) {
+    using namespace fastp;
+    if (!gplan) return;  // not used by this launch
+    // the header is read from global memory (uniform scalar loads)
+    np = gplan[kHNp]; nblk = gplan[kHNblk]; o_blk = gplan[kHBlk]; o_ls = gplan[kHLs]; o_site = gplan[kHSite];
+    o_siten = gplan[kHSiteN]; nops = gplan[kHNops]; centre_open = gplan[kHCentre];
+    lzp cb{(LDS double*)base};
+    MP = cb + gplan[kHZMps]; TH = cb + gplan[kHZTh]; TG = cb + gplan[kHZTg]; WB = cb + gplan[kHZW];
+    XS = cb + gplan[kHZX]; GT = cb + gplan[kHZGt]; PH = cb + gplan[kHZPh];
+    LDS double* db = (cb + gplan[kHZTot]).p;
+    LAM = db; SIG = db + 64;  // then 8 spare doubles
+    LDS int* ib = (LDS int*)(db + 136);
+    auto al = [](int x) { return (x + 3) & ~3; };  // 16-byte aligned int arrays
+    DIM = ib; ib += al(P.nsq);
+    BOF = ib; ib += al(nblk);
+    KQ = ib; ib += 64;
+    WIDX = ib; ib += 64;
+    ib += 4;  // flags (spare)
+    PL = ib;
+  }
+  __device__ __forceinline__ void wsync() const {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  __device__ __forceinline__ static i4 ld4(const LDS int* p) { return *(const LDS i4*)p; }
+  // plan image and gate tables into LDS (once per launch)
+  __device__ OCG_INLINE void init(const int* gplan, const zc* gf, const zc* gb) {
+    if (!act) return;
+    const int ni = gplan[fastp::kHNint];
+    for (int i = lane; i < ni; i += 64) PL[i] = gplan[i];
+    for (int i = lane; i < P.gtotal; i += 64) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
+    wsync();
+  }
+  __device__ __forceinline__ int dim(int b, int q) const { return (q < 0 || q > P.Q) ? 0 : DIM[b * P.Q1 + q]; }
+
+  // ------------------------------------------------------------- I/O
+  // compact interchange format (include/ocmps.h): dims[nsq], site k at
+  // site_base[k], blocks (q, n) packed row-major in (q, n) order.  BOF[b] =
+  // exclusive prefix of the compact block sizes over the block list (the
+  // site-relative offset is BOF[b] - BOF[first block of the site]); recomputed
+  // only after the dims changed.
+  __device__ OCG_INLINE void block_offsets() {
+    if (bof_epoch == dims_epoch) return;
+    int carry = 0;
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+      const int b = b0 + lane, bb = b < nblk ? b : nblk - 1;
+      const i4 t = ld4(PL + o_blk + 4 * bb);
+      const int sz = b < nblk ? DIM[t[1]] * DIM[t[2]] : 0;
+      const int inc = wscan(sz);
+      if (b < nblk) BOF[b] = carry + inc - sz;
+      carry += rdlane(inc, 63);
+    }
+    bof_epoch = dims_epoch;
+    wsync();
+  }
+  template <class PI, class PZ>
+  __device__ OCG_INLINE void load(const PI* gdims, const PZ* gdata) {
+    if (!act) return;
+    pf(10);
+    for (int i = lane; i < P.nsq; i += 64) DIM[i] = gdims[i];
+    ++dims_epoch;
+    wsync();
+    block_offsets();
+    i4 d[fastp::kItMps];
+#pragma unroll
+    for (int it = 0; it < fastp::kItMps; ++it) {
+      const int x = lane + 64 * it;
+      d[it] = ld4(PL + o_ls + 4 * (x < np ? x : np - 1));
+    }
+#pragma unroll
+    for (int it = 0; it < fastp::kItMps; ++it) {
+      const int x = lane + 64 * it;
+      const int dl = DIM[d[it][0] & 0xffff], dr = DIM[unsigned(d[it][0]) >> 16];
+      const int b = d[it][1] & 0xffff, f = unsigned(d[it][1]) >> 16, a = d[it][2] & 0xff, c = unsigned(d[it][2]) >> 8;
+      const bool ok = x < np && a < dl && c < dr;
+      const int idx = d[it][3] + BOF[b] - BOF[f] + a * dr + c;  // no lane-indexed kernel-argument read
+      zc v = c2(0.0, 0.0);
+      if (ok) v = c2(gdata[idx].x, gdata[idx].y);
+      if (x < np) MP[x] = v;
+    }
+    wsync();
+  }
+  // wt: write-through stores (agent-scope relaxed stores: the state leaves the
+  // XCD's L2 on the store itself, so a consumer on another XCD can read it after
+  // a flag without a release fence)
+  __device__ OCG_INLINE void store(int* gdims, zc* gdata, bool wt = false) {
+    if (!act) return;
+    pf(10);
+    block_offsets();
+    for (int i = lane; i < P.nsq; i += 64) {
+      if (wt) __hip_atomic_store(gdims + i, DIM[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else gdims[i] = DIM[i];
+    }
+    i4 d[fastp::kItMps];
+#pragma unroll
+    for (int it = 0; it < fastp::kItMps; ++it) {
+      const int x = lane + 64 * it;
+      d[it] = ld4(PL + o_ls + 4 * (x < np ? x : np - 1));
+    }
+#pragma unroll
+    for (int it = 0; it < fastp::kItMps; ++it) {
+      const int x = lane + 64 * it;
+      const int dl = DIM[d[it][0] & 0xffff], dr = DIM[unsigned(d[it][0]) >> 16];
+      const int b = d[it][1] & 0xffff, f = unsigned(d[it][1]) >> 16, a = d[it][2] & 0xff, c = unsigned(d[it][2]) >> 8;
+      const int idx = d[it][3] + BOF[b] - BOF[f] + a * dr + c;  // no lane-indexed kernel-argument read
+      const zc v = MP[x < np ? x : 0];
+      if (x < np && a < dl && c < dr) {
+        if (wt) {
+          double* dd = (double*)(gdata + idx);
+          __hip_atomic_store(dd, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dd + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          gdata[idx] = v;
+        }
+      }
+    }
+  }
+
+  __device__ OCG_INLINE void model_totals(double& b, double& f) const {
+    b = wsum(m_bytes);
+    f = wsum(m_flops);
+  }
+  // the traffic model of one two-site update on the current (unpadded) dims:
+  // 16 (2 (|A_i1| + |A_i2|) + gate) bytes, 8 (R C m + R C p + n^2 max(R, C) +
+  // 2 R C m) flops per middle sector (Chain::build_theta's accounting)
+  __device__ OCG_INLINE void model_gate(int i1) {
+    const int p = P.p, Q1 = P.Q1, q = lane;
+    double fl = 0.0, by = 0.0;
+    if (q < Q1) {
+      int R = 0, C = 0, u = 0;
+      const int m = dim(i1, q), dl = dim(i1 - 1, q);
+#pragma unroll
+      for (int n = 0; n < 6; ++n) {
+        if (n < p) {
+          R += dim(i1 - 1, q - n);
+          C += dim(i1 + 1, q + n);
+          u += dl * dim(i1, q + n) + m * dim(i1 + 1, q + n);
+        }
+      }
+      if (R == 0 || C == 0) { R = 0; C = 0; }
+      const double Rd = R, Cd = C, nn = R < C ? R : C;
+      fl = 8.0 * (Rd * Cd * m + Rd * Cd * p + nn * nn * (R > C ? Rd : Cd) + 2.0 * Rd * Cd * m);
+      by = 32.0 * double(u);
+    }
+    if (lane == 0) by += 16.0 * P.gtotal;
+    m_bytes += by;
+    m_flops += fl;
+  }
+
+  // ------------------------------------------------------------- Θ and gate
+  __device__ OCG_INLINE void theta(const LDS int* oh) {
+    using namespace fastp;
+    pf(0);
+    const int nth = oh[kOhNth];
+    const LDS int* md = PL + oh[kOhMat];
+    int d0[kItTh], d1[kItTh];
+#pragma unroll
+    for (int it = 0; it < kItTh; ++it) {
+      const int e = lane + 64 * it, ee = e < nth ? e : nth - 1;
+      d0[it] = md[2 * ee];
+      d1[it] = md[2 * ee + 1];
+    }
+#pragma unroll
+    for (int it = 0; it < kItTh; ++it) {
+      const int e = lane + 64 * it;
+      const int x1 = d0[it] & 0xffff, x2 = unsigned(d0[it]) >> 16, dm = d1[it] & 0xff, drc = unsigned(d1[it]) >> 8;
+      const int dmc = dm > 0 ? dm - 1 : 0;
+      zc acc = c2(0.0, 0.0);
+#pragma unroll
+      for (int b = 0; b < kMaxDm; ++b) {
+        const int bb = b < dmc ? b : dmc;
+        const zc a = MP[x1 + bb], v = MP[x2 + bb * drc];
+        if (b < dm) cacc(acc, a, v);
+      }
+      if (e < nth) TH[e] = acc;
+    }
+    wsync();
+  }
+  // pre-phase -> hopping gate (per Δ = n1 + n2 block) -> post-phase (Chain::apply_gate).
+  // PH holds UF[p], UT[p], then the pair products UF[n1] UF[n2] and UT[a1] UT[a2] (p^2 each)
+  __device__ OCG_INLINE void gate(const LDS int* oh, int forward) {
+    using namespace fastp;
+    pf(1);
+    const int p = P.p, nth = oh[kOhNth], mode = oh[kOhMode], lonely = oh[kOhLonely];
+    const LDS int* gd = PL + oh[kOhGate];
+    lzp g0 = GT + (forward ? 0 : P.gtotal);
+    lzp UF = PH, UT = PH + p, UFF = PH + 2 * p, UTT = PH + 2 * p + p * p;
+    i4 d[kItTh];
+#pragma unroll
+    for (int it = 0; it < kItTh; ++it) {
+      const int e = lane + 64 * it;
+      d[it] = ld4(gd + 4 * (e < nth ? e : nth - 1));
+    }
+#pragma unroll
+    for (int it = 0; it < kItTh; ++it) {
+      const int e = lane + 64 * it;
+      const unsigned h = d[it][0];
+      const int sz = (h >> 16) & 15, lo = (h >> 20) & 15, a1 = (h >> 24) & 15, a2 = h >> 28, D = a1 + a2;
+      lzp g = g0 + int(h & 0xffff);
+      zc acc = c2(0.0, 0.0);
+#pragma unroll
+      for (int x = 0; x < 6; ++x) {
+        const int xx = x < sz ? x : sz - 1;
+        const int n1 = lo + xx, n2 = D - n1;
+        const int ad = (unsigned(d[it][1 + (x >> 1)]) >> (16 * (x & 1))) & 0xffff;
+        zc z = TH[x < sz ? ad : 0];
+        const zc ph = mode == 0 ? zc(UFF[n1 * p + n2]) : zc(UF[n2]);
+        if (mode == 0 || (lonely & 2)) z = cmul(z, ph);
+        const zc gx = g[xx];
+        if (x < sz) cacc(acc, gx, z);
+      }
+      const zc po = mode == 1 ? zc(UTT[a1 * p + a2]) : zc(UT[a2]);
+      if (mode == 1 || (lonely & 1)) acc = cmul(acc, po);
+      if (e < nth) TG[e] = acc;
+    }
+    wsync();
+  }
+  // single-site matricisation (gauge moves): M[e] = A[src[e]]
+  __device__ OCG_INLINE void matcopy(const LDS int* oh) {
+    using namespace fastp;
+    pf(7);
+    const int nth = oh[kOhNth];
+    const LDS int* src = PL + oh[kOhMat];
+    int s[kItTh];
+#pragma unroll
+    for (int it = 0; it < kItTh; ++it) {
+      const int e = lane + 64 * it;
+      s[it] = src[e < nth ? e : nth - 1];
+    }
+#pragma unroll
+    for (int it = 0; it < kItTh; ++it) {
+      const int e = lane + 64 * it;
+      const zc v = MP[s[it]];
+      if (e < nth) TH[e] = v;
+    }
+    wsync();
+  }
+
+  // ------------------------------------------------------------- decomposition
+  // Block decomposition of M (ITensor denmatDecomp per QN block, global
+  // truncation): Gram on the smaller side of each block, register Jacobi for
+  // orders 2..4, the truncation rule, factors into their destinations; the
+  // rewritten bond's dims.  normalize: the norm-carrying factor divided by
+  // sqrt(kept weight) (doStep's centre normalisation).
+  __device__ OCG_INLINE void decompose(const LDS int* oh, lzp M, int dir, double cutoff, int maxm, bool normalize) {
+    using namespace fastp;
+    pf(2);
+    const int nsec = oh[kOhNsec], T = oh[kOhT], maxr = oh[kOhMaxr], no1 = oh[kOhNo1];
+    // ---- Gram of the Jacobi groups: lane 16 g + 4 i + j holds G[i][j]
+    const int g = lane >> 4, i = (lane >> 2) & 3, j = lane & 3, rb = lane & ~15;
+    const i4 ga = ld4(oh + kOhGrp + 8 * g), gb = ld4(oh + kOhGrp + 8 * g + 4);
+    const bool used = ga[0] >= 0;
+    const int n = used ? ga[1] : 0, side = ga[2], tho = ga[3], R = gb[0], C = gb[1], eoff = gb[2];
+    const bool valid = i < n && j < n;
+    // order-1 sectors (lanes < no1): the block's one row / column squared norm
+    const i4 o1 = ld4(PL + oh[kOhO1] + 4 * (lane < no1 ? lane : 0));
+    zc gv = c2(0.0, 0.0);
+    double lam1 = 0.0;
+    {
+      const int len = used ? (side == 0 ? C : R) : 0, st = side == 0 ? 1 : C;
+      const int bi = side == 0 ? tho + (i < n ? i : 0) * C : tho + (i < n ? i : 0);
+      const int bj = side == 0 ? tho + (j < n ? j : 0) * C : tho + (j < n ? j : 0);
+      const int lc = len > 0 ? len - 1 : 0;
+      const int len1 = lane < no1 ? o1[1] : 0;
+      const int l1 = len1 > 0 ? len1 - 1 : 0;
+#pragma unroll
+      for (int c = 0; c < kMaxDot; ++c) {
+        const int cc = c < lc ? c : lc;
+        const zc a = M[used ? bi + cc * st : 0], b = M[used ? bj + cc * st : 0];
+        const int c1 = c < l1 ? c : l1;
+        const zc z1 = M[len1 > 0 ? o1[0] + c1 * o1[2] : 0];
+        if (c < len) {
+          if (side == 0) cacc(gv, a, cconj(b));
+          else cjacc(gv, a, b);
+        }
+        if (c < len1) lam1 += cabs2(z1);
+      }
+    }
+    if (!valid) gv = c2(0.0, 0.0);
+    zc w = c2(i == j ? 1.0 : 0.0, 0.0);
+    pf(3);
+    if (maxr > 0) jacobi(gv, w, valid, i, j, rb, n, maxr);
+    pf(4);
+    // eigenvectors and eigenvalues (clamped at 0) to LDS
+    if (used) WB[16 * g + 4 * i + j] = w;
+    if (valid && i == j) LAM[eoff + i] = gv.x > 0 ? gv.x : 0.0;
+    if (lane < no1) LAM[o1[3]] = lam1;
+    wsync();
+    // ---- truncation (Chain::decompose, one-wave form): eigen slot e = lane
+    const bool ae = lane < T;
+    const i4 eq = ld4(PL + oh[kOhEq] + 4 * (ae ? lane : 0));
+    const double lam = ae ? LAM[lane] : 0.0;
+    const int s_e = eq[0], i_e = eq[1], eo_e = eq[2], n_e = eq[3] & 255, bound = unsigned(eq[3]) >> 8;
+    // rank inside the block (descending, ties by index)
+    int jb = 0;
+#pragma unroll
+    for (int t = 0; t < kMaxGram; ++t) {
+      const double lt = CH::bperm(lam, ((eo_e + t) & 63) << 2);
+      jb += (ae && t < n_e && t != i_e && (lt > lam || (lt == lam && t < i_e))) ? 1 : 0;
+    }
+    const double total = wsum(lam);
+    const double cut = cutoff * total, floor_ = 1e-30 * total;
+    bool disc = false;
+    if (T <= maxm) {
+      // Maxm cannot bind: only eigenvalues below max(cut, floor) can be discarded
+      const double thr = fmax(cut, floor_);
+      const bool small = ae && (lam < thr || lam <= floor_);
+      unsigned long long Mk = __ballot(small);
+      if (Mk) {
+        const int nbig = T - __popcll(Mk);
+        double S = lam;
+        int rs = 0;
+        while (Mk) {
+          const int f = __ffsll((long long)Mk) - 1;
+          Mk &= Mk - 1;
+          const double lf = rdlane(lam, f);
+          rs += (lf > lam || (lf == lam && f < lane)) ? 1 : 0;
+          if (f != lane && (lf < lam || (lf == lam && f > lane))) S += lf;
+        }
+        disc = small && nbig + rs >= 1 && (S < cut || lam <= floor_);
+      }
+    } else {
+      // global rank (descending; ties by slot), then the sorted spectrum's suffix sums
+      int rk = 0;
+      for (int f = 0; f < T; ++f) {
+        const double lf = rdlane(lam, f);
+        rk += (lf > lam || (lf == lam && f < lane)) ? 1 : 0;
+      }
+      // lane T-1-rk receives lam: lanes ascend from the smallest
+      const int dst = ((T - 1 - rk) & 63) << 2;
+      const long long lb = __double_as_longlong(lam);
+      const unsigned lo = unsigned(__builtin_amdgcn_ds_permute(dst, int(lb)));
+      const unsigned hi = unsigned(__builtin_amdgcn_ds_permute(dst, int(lb >> 32)));
+      const double v = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+      const int jpos = T - 1 - lane;  // sorted position of the value lane holds
+      const double vv = lane < T ? v : 0.0;
+      const double suf = wscan(vv);
+      const bool d2 = lane < T && jpos >= 1 && (jpos >= maxm || suf < cut || vv <= floor_);
+      // discarded positions are a suffix of the sorted order: m = kept count
+      const int m = T - __popcll(__ballot(d2));
+      disc = ae && rk >= m;
+    }
+    const bool kept = ae && !disc && jb < bound;
+    if (kept) {
+      WIDX[eo_e + jb] = i_e;
+      SIG[eo_e + jb] = sqrt(lam);
+    }
+    const double kw = wsum(kept ? lam : 0.0);
+    int kq = 0;
+    for (int s = 0; s < nsec; ++s) {
+      const int c = __popcll(__ballot(kept && s_e == s));
+      kq = (lane == s) ? c : kq;
+    }
+    {
+      const int newb = oh[kOhNewBond];
+      const int q = lane < nsec ? PL[oh[kOhSecQ] + lane] : 0;
+      bool changed = false;
+      if (lane < nsec) {
+        const int at = newb * P.Q1 + q;
+        changed = DIM[at] != kq;
+        KQ[lane] = kq;
+        DIM[at] = kq;
+      }
+      if (__ballot(changed)) ++dims_epoch;
+    }
+    wsync();
+    pf(5);
+    // ---- factors (Chain::decompose's materialisation): X rows, Y cols
+    const double inv = (normalize && kw > 1e-32) ? 1.0 / sqrt(kw) : 1.0;
+    const int nf = oh[kOhNf];
+    const LDS int* fl = PL + oh[kOhF];
+    i4 fd[kItF];
+#pragma unroll
+    for (int it = 0; it < kItF; ++it) {
+      const int e = lane + 64 * it;
+      fd[it] = ld4(fl + 4 * (e < nf ? e : nf - 1));
+    }
+    zc out[kItF];
+    int dst[kItF];
+#pragma unroll
+    for (int it = 0; it < kItF; ++it) {
+      const int e = lane + 64 * it;
+      const int w0 = fd[it][0], w1 = fd[it][1], w2 = fd[it][2], wbse = fd[it][3];
+      const int dest = w0 & 0xffff, s = (w0 >> 16) & 15, jj = (w0 >> 20) & 15;
+      const bool isx = (w0 >> 24) & 1, scr = (w0 >> 25) & 1;
+      const int eo = w2 & 255, ns = (w2 >> 8) & 15;
+      const bool exact = (w2 >> 12) & 1;
+      const int kqs = KQ[s], wv = WIDX[eo + jj];
+      const double sig = SIG[eo + jj];
+      const bool live = jj < kqs && e < nf;
+      const int wvc = live ? wv : 0;
+      zc r = c2(0.0, 0.0);
+      if (exact) {
+        const zc wx = ns == 1 ? c2(1.0, 0.0) : zc(WB[w1 + wvc]);
+        r = isx ? wx : cconj(wx);
+        if (isx ? dir == kFromright : dir == kFromleft) r = cscale(r, sig * inv);
+      } else {
+        const int mb = w1 & 0xffff, terms = (w1 >> 16) & 31, ms = unsigned(w1) >> 21;
+        const int tc = terms > 0 ? terms - 1 : 0;
+        zc acc = c2(0.0, 0.0);
+#pragma unroll
+        for (int x = 0; x < kMaxGram; ++x) {
+          const int xx = x < tc ? x : tc;
+          const zc mv = M[mb + xx * ms];
+          const zc wx = ns == 1 ? c2(1.0, 0.0) : zc(WB[(wbse > 0 ? wbse : 0) + 4 * xx + wvc]);
+          if (x < terms) {
+            if (isx) cacc(acc, mv, wx);  // Θ w
+            else cjacc(acc, wx, mv);     // w^H Θ
+          }
+        }
+        const bool orth = isx ? dir == kFromleft : dir == kFromright;  // the orthonormal side divides by sigma
+        r = orth ? (sig > 0 ? cscale(acc, 1.0 / sig) : c2(0.0, 0.0)) : cscale(acc, inv);
+      }
+      out[it] = live ? r : c2(0.0, 0.0);
+      dst[it] = e < nf ? (dest | (scr ? 0x10000 : 0)) : -1;
+    }
+#pragma unroll
+    for (int it = 0; it < kItF; ++it)
+      if (dst[it] >= 0) ((dst[it] >> 16) ? XS : MP)[dst[it] & 0xffff] = out[it];
+    wsync();
+  }
+
+  // register Jacobi on up to four Gram blocks of order <= 4 (Chain::jacobi_reg<4>):
+  // lane 16 g + 4 i + j holds G[i][j] and W[i][j] of group g; round r pairs
+  // x with x ^ (r + 1), partner elements by DPP, rotations by bpermute.  The
+  // lane also carries the diagonal entries of its row and column (di, dj),
+  // updated by the rotations' shifts, so a round needs no diagonal gather.
+  __device__ OCG_INLINE void jacobi(zc& g, zc& w, bool valid, int i, int j, int rb, int n, int maxr) {
+    auto at = [&](int r, int c) { return (rb + r * 4 + c) << 2; };
+    double di = CH::bperm(g.x, at(i, i)), dj = CH::bperm(g.x, at(j, j));
+    int arow[3], acol[3], fl[3];
+#pragma unroll
+    for (int rnd = 0; rnd < 3; ++rnd) {
+      const int k = rnd + 1;
+      int pi = i, pj = j;
+      if (rnd < maxr && valid) {
+        if ((i ^ k) < n) pi = i ^ k;
+        if ((j ^ k) < n) pj = j ^ k;
+      }
+      arow[rnd] = at(i < pi ? i : pi, i < pi ? pi : i);
+      acol[rnd] = at(j < pj ? j : pj, j < pj ? pj : j);
+      fl[rnd] = (i < j && pi == j ? 1 : 0) | (j < pj ? 2 : 0) | (i < pi ? 4 : 0) | (pj != j ? 8 : 0) |
+                (pi != i ? 16 : 0) | (pi == j ? 32 : 0);
+    }
+    int sweep = 0;
+    bool done = false;
+    for (; sweep < 40; ++sweep) {
+      bool flag = false;
+#pragma unroll
+      for (int rnd = 0; rnd < 3; ++rnd) {
+        if (rnd >= maxr) break;
+        const int f = fl[rnd];
+        const bool need = CH::jneed(cabs2(g), di, dj);
+        if (__ballot(valid && i < j && need) == 0) {
+          done = true;
+          break;
+        }
+        zc cs, e;
+        double sh;
+        CH::jrot_fast(g, di, dj, need, cs, e, sh);
+        const bool piv = f & 1;
+        cs = piv ? cs : c2(1.0, 0.0);
+        sh = piv ? sh : 0.0;
+        const zc csj = CH::bpermz(cs, acol[rnd]), ej = CH::bpermz(e, acol[rnd]);
+        const zc csi = CH::bpermz(cs, arow[rnd]), ei = CH::bpermz(e, arow[rnd]);
+        const double shj = CH::bperm(sh, acol[rnd]), shi = CH::bperm(sh, arow[rnd]);
+        const zc g01 = CH::xcol(g, rnd), g10 = CH::xrow(g, rnd);
+        const zc g11 = CH::xrow(g01, rnd), w1 = CH::xcol(w, rnd);
+        const bool rotj = (f & 8) && csj.y != 0.0, roti = (f & 16) && csi.y != 0.0;
+        zc jjj, jpj, jii, jpi;
+        CH::jcol(f & 2, csj, ej, jjj, jpj);
+        CH::jcol(f & 4, csi, ei, jii, jpi);
+        jjj = rotj ? jjj : c2(1, 0);
+        jpj = rotj ? jpj : c2(0, 0);
+        jii = roti ? jii : c2(1, 0);
+        jpi = roti ? jpi : c2(0, 0);
+        zc wn = cmul(w, jjj);
+        cacc(wn, w1, jpj);
+        zc r0 = cmul(g, jjj);
+        cacc(r0, g01, jpj);
+        zc r1 = cmul(g10, jjj);
+        cacc(r1, g11, jpj);
+        zc out = cjmul(jii, r0);
+        cjacc(out, jpi, r1);
+        const bool zero = rotj && roti && (f & 32);
+        const bool diag = rotj && i == j;
+        out = zero ? c2(0, 0) : out;
+        out = diag ? c2(g.x + ((f & 2) ? -shj : shj), 0) : out;
+        // the diagonal entries of this lane's row and column after the rotation
+        const double dj2 = rotj ? dj + ((f & 2) ? -shj : shj) : dj;
+        const double di2 = roti ? di + ((f & 4) ? -shi : shi) : di;
+        if (rnd == maxr - 1) flag = valid && i < j && CH::jneed(cabs2(out), di2, dj2);
+        g = out;
+        w = wn;
+        di = di2;
+        dj = dj2;
+      }
+      if (done || __ballot(flag) == 0) break;
+    }
+    if (sweep == 40 && lane == 0 && P.err) atomicOr(P.err, OCG_ERR_JACOBI);
+  }
+
+  // ------------------------------------------------------------- gauge neighbour
+  // right move: A_{k+1} <- Y A_{k+1}; left move: A_{k-1} <- A_{k-1} X (XS holds the factor)
+  __device__ OCG_INLINE void neighbour(const LDS int* oh) {
+    using namespace fastp;
+    pf(25);
+    const int ns = oh[kOhNs], kind = oh[kOhKind];
+    const LDS int* sl = PL + oh[kOhS];
+    i4 d[kItS];
+#pragma unroll
+    for (int it = 0; it < kItS; ++it) {
+      const int e = lane + 64 * it;
+      d[it] = ld4(sl + 4 * (e < ns ? e : ns - 1));
+    }
+    zc acc[kItS];
+#pragma unroll
+    for (int it = 0; it < kItS; ++it) {
+      const int x1 = d[it][0] & 0xffff, x2 = unsigned(d[it][0]) >> 16, len = d[it][1] & 0xffff,
+                s2 = unsigned(d[it][1]) >> 16;
+      const int lc = len > 0 ? len - 1 : 0;
+      acc[it] = c2(0.0, 0.0);
+#pragma unroll
+      for (int b = 0; b < kMaxDm; ++b) {
+        const int bb = b < lc ? b : lc;
+        const zc a = (kind == kOpGaugeR) ? zc(XS[x1 + bb]) : zc(MP[x1 + bb]);
+        const zc v = (kind == kOpGaugeR) ? zc(MP[x2 + bb * s2]) : zc(XS[x2 + bb * s2]);
+        if (b < len) cacc(acc[it], a, v);
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int it = 0; it < kItS; ++it)
+      if (lane + 64 * it < ns) MP[d[it][2]] = acc[it];
+    wsync();
+  }
+
+  // ------------------------------------------------------------- step
+  // BH_tDMRG::step (src/BH_tDMRG.cpp:111-125) + doStep (:127-230), as Chain::step
+  // (final_gauge = false: the closing position(1) is skipped, the centre stays on
+  // the last gate's left site, which is normalised instead of site 1).
+  __device__ OCG_INLINE void step(double ufrom, double uto, int forward, bool final_gauge = true) {
+    using namespace fastp;
+    if (!act) return;
+    pf(29);
+    const int p = P.p;
+    const double tau = forward ? P.dt : -P.dt;
+    if (lane < p) {  // U phases exp(-i u tau n(n-1) / 4) (initUGates, :74-108)
+      const double nn = double(lane) * double(lane - 1);
+      double s, c;
+      zc f;
+      if (ufrom == ph_u && forward == ph_dir) {
+        f = PH[p + lane];
+      } else {
+        sincos(-0.25 * ufrom * tau * nn, &s, &c);
+        f = c2(c, s);
+      }
+      PH[lane] = f;
+      sincos(-0.25 * uto * tau * nn, &s, &c);
+      PH[p + lane] = c2(c, s);
+    }
+    ph_u = uto;
+    ph_dir = forward;
+    wsync();
+    for (int x = lane; x < p * p; x += 64) {  // pair products UF[n1] UF[n2], UT[a1] UT[a2]
+      const int a = x / p, b = x - a * p;
+      PH[2 * p + x] = cmul(PH[a], PH[b]);
+      PH[2 * p + p * p + x] = cmul(PH[p + a], PH[p + b]);
+    }
+    wsync();
+    for (int o = 0; o < nops; ++o) {
+      const LDS int* oh = PL + PL[kHOps + o];
+      const i4 h0 = ld4(oh), h1 = ld4(oh + 4);
+      if (h1[1] && !final_gauge) continue;  // closing move
+      const int kind = h0[0], dir = h0[2];
+      if (kind == kOpGate) {
+        pf(12);
+        model_gate(h0[1]);
+        theta(oh);
+        gate(oh, forward);
+        decompose(oh, TG, dir, P.cutoff, P.maxm, true);
+      } else {
+        matcopy(oh);
+        decompose(oh, TH, dir, OCG_GAUGE_CUTOFF, 1 << 30, false);
+        neighbour(oh);
+      }
+    }
+    // lonely U_to on site 1 (:222-223), then psi.normalize() (:228): the norm of
+    // the MPS is the norm of the centre site
+    pf(9);
+    const int centre = final_gauge ? 1 : centre_open;
+    const int s1a = PL[o_site + 1], s1b = PL[o_site + 2];
+    for (int x = s1a + lane; x < s1b; x += 64) MP[x] = cmul(MP[x], PH[p + PL[o_siten + x - s1a]]);
+    wsync();
+    const int ca = PL[o_site + centre], cb = PL[o_site + centre + 1];
+    double acc = 0.0;
+    zc v[kItMps];
+#pragma unroll
+    for (int it = 0; it < kItMps; ++it) {
+      const int x = ca + lane + 64 * it;
+      v[it] = MP[x < cb ? x : ca];
+      if (x < cb) acc += cabs2(v[it]);
+    }
+    const double n2 = wsum(acc);
+    if (n2 > 0) {
+      const double f = 1.0 / sqrt(n2);
+#pragma unroll
+      for (int it = 0; it < kItMps; ++it) {
+        const int x = ca + lane + 64 * it;
+        if (x < cb) MP[x] = cscale(v[it], f);
+      }
+    }
+    wsync();
+  }
+};
+
+}  // namespace ocg

@@ -4,8 +4,30 @@
 #pragma once
 
 #include "engine_device.hpp"
+#include "fast_chain.hpp"
 
 namespace ocg {
+
+// LDS arrays of the general chain as flat pointers (the one-wave chain's
+// load / store take either global or LDS memory)
+__device__ __forceinline__ int* flat(LDS int* p) { return (int*)p; }
+__device__ __forceinline__ zc* flat(lzp p) { return (zc*)(double*)p.p; }
+// the one-wave padded chain steps this launch (fast_chain.hpp)
+__device__ __forceinline__ bool fast_on(const OcgParams& P) { return P.fplan != nullptr && !P.imag; }
+// a publishing fast chain's write-through stores have all completed (wave 0; the
+// other waves store nothing), so the flag that follows can be a plain relaxed
+// agent-scope store: no L2 write-back fence (MI355X_MICROARCH.md, hand-off table)
+__device__ __forceinline__ void publish_flag_wt(int* flag, int epoch, int* progress) {
+  if (threadIdx.x < 64) {
+#ifndef OCG_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(progress, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // --------------------------------------------------------------------------
 // device statistics: [kind][0] = alg bytes, [1] = alg flops, [2] = steps
@@ -59,16 +81,31 @@ __device__ OCG_INLINE void body_trajectory(char* smem, OcgParams P, const zc* gf
   const int base = fwd ? psi_base : xi_base;
   const int src = fwd ? slot_init : slot_target;
   double bytes = 0, flops = 0;
-  c.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
   int t = fwd ? 0 : N - 1;
-  c.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
-  for (int s = 0; s + 1 < N; ++s) {
-    const int tn = fwd ? t + 1 : t - 1;
-    c.step(u[t], u[tn], fwd, s + 2 == N);  // closing gauge move on the last step only (Chain::step)
-    c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
-    t = tn;
+  if (fast_on(P)) {
+    FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+    f.init(P.fplan, gf, gb);
+    f.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
+    f.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
+    for (int s = 0; s + 1 < N; ++s) {
+      const int tn = fwd ? t + 1 : t - 1;
+      f.step(u[t], u[tn], fwd, s + 2 == N);
+      f.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
+      t = tn;
+    }
+    f.model_totals(bytes, flops);
+    __syncthreads();
+  } else {
+    c.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
+    c.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
+    for (int s = 0; s + 1 < N; ++s) {
+      const int tn = fwd ? t + 1 : t - 1;
+      c.step(u[t], u[tn], fwd, s + 2 == N);  // closing gauge move on the last step only (Chain::step)
+      c.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn));
+      t = tn;
+    }
+    c.model_totals(bytes, flops);
   }
-  c.model_totals(bytes, flops);
   flush_stats(c, stats, bytes, flops, double(N - 1));
 }
 
@@ -122,9 +159,26 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
   const double normiH = norms[i];
   c.load(SLOT_D(pool, P, psih_base + i), SLOT_X(pool, P, psih_base + i));
   double bytes = 0, flops = 0;
+  const bool fo = fast_on(P);
+  FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+  if (fo) {
+    f.init(P.fplan, gf, gb);
+    f.load(SLOT_D(pool, P, psih_base + i), SLOT_X(pool, P, psih_base + i));
+  }
   // j = i: diagonal entry (:259-264); j > i: step psiH once, then overlap (:266-278)
   for (int j = i; j + 1 < N; ++j) {
-    if (j > i) c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
+    if (j > i) {
+      if (fo) {
+        // the one-wave chain steps; its state goes through the general chain's
+        // LDS copy (compact layout, offsets rebuilt by load) for the overlap
+        f.step(u[j - 1], u[j], 1, false);
+        f.store(flat(c.DIMS), flat(c.A));
+        __syncthreads();
+        c.load(flat(c.DIMS), flat(c.A));
+      } else {
+        c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
+      }
+    }
     zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
     const double used = c.mps_used();
     if (threadIdx.x == 0) {
@@ -138,7 +192,8 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
     }
   }
   double mb, mf;
-  c.model_totals(mb, mf);
+  if (fo) f.model_totals(mb, mf);
+  else c.model_totals(mb, mf);
   bytes += mb;
   flops += mf;
   flush_stats(c, stats, bytes, flops, double(N - 2 - i > 0 ? N - 2 - i : 0));
@@ -229,6 +284,34 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
   c.load_tables(gf, gb, md);
   int* const progress = flags + 2 * N;
   double bytes = 0, flops = 0, nsteps = 0;
+  const bool fo = fast_on(P);
+  FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+  if (fo && (b < 2 || b >= 2 + nxw)) f.init(P.fplan, gf, gb);
+  if (b < 2 && fo) {
+    // calcPsi / calcXi on the one-wave chain: every state stored write-through;
+    // state t's flag is raised after step t+1 has been computed, when its
+    // stores have long completed (the wait costs nothing on the chain's path)
+    const int fwd = (b == 0) ? 1 : 0;
+    const int base = fwd ? psi_base : xi_base;
+    int* fl = flags + (fwd ? 0 : N);
+    const int src = fwd ? slot_init : slot_target;
+    f.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
+    int t = fwd ? 0 : N - 1;
+    f.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t), true);
+    for (int s = 0; s + 1 < N; ++s) {
+      const int tn = fwd ? t + 1 : t - 1;
+      f.step(u[t], u[tn], fwd, s + 2 == N);
+      publish_flag_wt(fl + t, epoch, progress);
+      f.store(SLOT_D(pool, P, base + tn), SLOT_X(pool, P, base + tn), true);
+      t = tn;
+    }
+    publish_flag_wt(fl + t, epoch, progress);
+    nsteps = N - 1;
+    f.model_totals(bytes, flops);
+    __syncthreads();
+    flush_stats(c, stats, bytes, flops, nsteps);
+    return;
+  }
   if (b < 2) {
     // calcPsi / calcXi (src/OptimalControl.cpp:375-407), every state published
     const int fwd = (b == 0) ? 1 : 0;
@@ -269,15 +352,30 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     if (threadIdx.x == 0) rnorm0[(size_t)kc * nrows + r] = sqrt(n2);
     int k = kc * rbase[nrows] + rbase[r];  // control kc's row states follow control kc-1's
     c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
-    for (int j = i + 1; j + 1 < N; ++j) {  // timeStepper.step(psiH, u[j-1], u[j]) (:269)
-      c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
-      ++k;
-      c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
+    if (fo) {  // the row's steps on the one-wave chain, from the general chain's LDS copy
+      f.load(flat(c.DIMS), flat(c.A));
+      for (int j = i + 1; j + 1 < N; ++j) {
+        f.step(u[j - 1], u[j], 1, false);
+        ++k;
+        f.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
+      }
+      double fb, ff;
+      f.model_totals(fb, ff);
+      bytes += fb;
+      flops += ff;
+      __syncthreads();
+    } else {
+      for (int j = i + 1; j + 1 < N; ++j) {  // timeStepper.step(psiH, u[j-1], u[j]) (:269)
+        c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
+        ++k;
+        c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
+      }
     }
     nsteps = N - 2 - i;
   }
-  c.model_totals(bytes, flops);
-  flush_stats(c, stats, bytes, flops, nsteps);
+  double mb, mf;
+  c.model_totals(mb, mf);
+  flush_stats(c, stats, bytes + mb, flops + mf, nsteps);
 }
 
 // H_ij from the stored psiH_i(j) (calcHessianRow's two terms, :259-277)
@@ -333,9 +431,20 @@ __device__ OCG_INLINE void body_steps(char* smem, OcgParams P, const zc* gf, con
   c.load_tables(gf, gb, md);
   int i = blockIdx.x;
   if (i >= n) return;
-  c.load(SLOT_D(pool, P, slots[i]), SLOT_X(pool, P, slots[i]));
   double bytes = 0, flops = 0;
   const double* ui = u + (size_t)i * u_stride;
+  if (fast_on(P)) {
+    FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+    f.init(P.fplan, gf, gb);
+    f.load(SLOT_D(pool, P, slots[i]), SLOT_X(pool, P, slots[i]));
+    for (int s = 0; s < nsteps; ++s) f.step(ui[s], ui[s + 1], forward);
+    f.store(SLOT_D(pool, P, slots[i]), SLOT_X(pool, P, slots[i]));
+    f.model_totals(bytes, flops);
+    __syncthreads();
+    flush_stats(c, stats, bytes, flops, double(nsteps));
+    return;
+  }
+  c.load(SLOT_D(pool, P, slots[i]), SLOT_X(pool, P, slots[i]));
   for (int s = 0; s < nsteps; ++s) {
     c.step(ui[s], ui[s + 1], forward);
   }

@@ -22,6 +22,7 @@
 #include "hbm.hpp"
 #include "engine_device.hpp"
 #include "params.hpp"
+#include "fast_plan.hpp"
 
 using ocg::Chain;
 using ocg::zc;
@@ -165,6 +166,7 @@ struct ocg_ctx {
   // parameter block of the overlap-only kernels
   OcgParams Po() const {
     OcgParams q = P;
+    q.fplan = nullptr;
     q.nplan = 0;
     q.plan_pe = 0;
     q.lds_bytes = lds_ovl;
@@ -175,6 +177,7 @@ struct ocg_ctx {
   int plan_pe2 = 0, lds2 = 0;
   OcgParams P2() const {
     OcgParams q = P;
+    if (P.fplan) return q;  // the one-wave chain's region follows the plan-less layout (one chain per CU)
     if (plan_pe2 >= 32) {
       q.plan_pe = plan_pe2;
       q.lds_bytes = lds2;
@@ -188,6 +191,7 @@ struct ocg_ctx {
   // parameter block of those kernels: plans off, smaller LDS
   OcgParams Pn() const {
     OcgParams q = P;
+    q.fplan = nullptr;
     q.nplan = 0;
     q.plan_pe = 0;
     q.lds_bytes = lds_np;
@@ -240,6 +244,8 @@ struct ocg_ctx {
   int pc_cap = 0;
   double* d_prn = nullptr;    // psiH norms by row slot
   int prn_cap = 0;
+  int* d_fplan = nullptr;     // plan image of the one-wave padded chain (null: off)
+  std::string fast_why;       // why it is off
   // trajectory state
   int N = 0;
   std::vector<double> u_psi, u_xi;  // controls of the device psi_t / xi_t (empty: none)
@@ -507,6 +513,39 @@ static int finish_params(ocg_ctx* c) {
     return fail(c, OCG_ECAP,
                 "chain workgroup needs " + std::to_string(l.bytes) + " B of LDS (> " + std::to_string(limit) +
                     "): configuration exceeds the single-workgroup engine (see DESIGN.md §Scope)");
+  // the one-wave padded chain (fast_chain.hpp) for every step when the
+  // configuration fits it (OCG_NO_FAST=1: the general chain steps, A/B and tests);
+  // its region follows the plan-less layout, whose decompositions (exactApplyMPO,
+  // the ground state) need no plans
+  c->P.fplan = nullptr;
+  c->P.fast_off = 0;
+  const char* nf = std::getenv("OCG_NO_FAST");
+  if (nf && nf[0] && nf[0] != '0') {
+    c->fast_why = "OCG_NO_FAST";
+    return 0;
+  }
+  ocg_host::FastPlanBuild fb = ocg_host::build_fast_plan(c->P, c->md);
+  if (!fb.why_not.empty()) {
+    c->fast_why = fb.why_not;
+    return 0;
+  }
+  const int off = (l.bytes + 255) & ~255;
+  const int fbytes = ocg_host::fast_lds_bytes(fb.plan, c->P);
+  if (size_t(off + fbytes) > limit) {
+    c->fast_why = "LDS";
+    return 0;
+  }
+  HIPCHK(c, hipMalloc(&c->d_fplan, sizeof(int) * fb.plan.size()));
+  HIPCHK(c, hipMemcpyAsync(c->d_fplan, fb.plan.data(), sizeof(int) * fb.plan.size(), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->P.fplan = c->d_fplan;
+  c->P.fast_off = off;
+  c->P.nplan = 0;
+  c->P.plan_pe = 0;
+  c->P.lds_bytes = off + fbytes;
+  c->plan_pe2 = 0;
+  c->lds2 = 0;
   return 0;
 }
 
@@ -690,6 +729,7 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->d_norms) (void)hipFree(c->d_norms);
   if (c->d_rnorm) (void)hipFree(c->d_rnorm);
   if (c->d_idx2) (void)hipFree(c->d_idx2);
+  if (c->d_fplan) (void)hipFree(c->d_fplan);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   for (auto& e : c->evh)
     if (e) (void)hipEventDestroy(e);
@@ -707,6 +747,7 @@ int ocg_get_info(const ocg_ctx* c, ocg_info* info) {
     info->lds_bytes = 0;
     info->block_threads = 256;
     info->device = c->device;
+    info->fast_chain = 0;
     return 0;
   }
   info->L = c->P.L; info->p = c->P.p; info->Q = c->P.Q;
@@ -714,6 +755,7 @@ int ocg_get_info(const ocg_ctx* c, ocg_info* info) {
   info->lds_bytes = c->P.lds_bytes;
   info->block_threads = NT;
   info->device = c->device;
+  info->fast_chain = c->P.fplan != nullptr;
   return 0;
 }
 

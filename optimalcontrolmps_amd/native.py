@@ -43,7 +43,8 @@ def build_native(force: bool = False, nt: int | None = None, verbose: bool = Fal
     if nt:
         flags.append(f"-DOCG_NT={int(nt)}")
     deps = {
-        "ocmps": ["ocmps.hip", "engine.hpp", "engine_device.hpp", "kernels.hpp", "params.hpp", "hbm.hpp"],
+        "ocmps": ["ocmps.hip", "engine.hpp", "engine_device.hpp", "kernels.hpp", "params.hpp", "hbm.hpp",
+                  "fast.hpp", "fast_plan.hpp", "fast_chain.hpp"],
         "hbm": ["hbm.hip", "hbm.hpp", "hbm_device.hpp", "hbm_eig.hpp"],
     }
     tag = f"nt{int(nt)}" if nt else "prod"
@@ -79,7 +80,7 @@ szp = C.POINTER(C.c_size_t)
 
 class OcgInfo(C.Structure):
     _fields_ = [("L", C.c_int), ("p", C.c_int), ("Q", C.c_int), ("mps_max_nelem", C.c_size_t),
-                ("lds_bytes", C.c_int), ("block_threads", C.c_int), ("device", C.c_int)]
+                ("lds_bytes", C.c_int), ("block_threads", C.c_int), ("device", C.c_int), ("fast_chain", C.c_int)]
 
 
 # (name, restype, argtypes) for every entry point of include/ocmps.h

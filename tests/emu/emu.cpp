@@ -13,8 +13,9 @@
 #include "hip/hip_runtime.h"
 #include "../../optimalcontrolmps_amd/csrc/kernels.hpp"
 #include "../../optimalcontrolmps_amd/csrc/params.hpp"
+#include "../../optimalcontrolmps_amd/csrc/fast_plan.hpp"
 
-thread_local emu_dim3 threadIdx, blockIdx;
+thread_local emu_dim3 threadIdx, blockIdx, gridDim;
 thread_local std::barrier<>* emu_bar;
 thread_local std::barrier<>* emu_wbar;
 thread_local uint64_t* emu_xbuf;
@@ -27,6 +28,7 @@ constexpr int NT = EMU_NT;
 struct Emu {
   OcgParams P;
   std::vector<int> md;
+  std::vector<int> fplan;  // one-wave padded chain plan (empty: off)
   std::vector<double> gf, gb;
   int lds = 0;
   std::vector<int> dims;       // pool
@@ -56,6 +58,7 @@ static void launch(Emu& e, int grid, const std::function<void(char*)>& body) {
       th.emplace_back([&, t, b]() {
         threadIdx.x = t;
         blockIdx.x = b;
+        gridDim.x = grid;
         emu_bar = &bar;
         emu_wbar = wb[t / 64].get();
         emu_xbuf = xb.data();
@@ -111,6 +114,25 @@ void* emu_new(int L, int p, int Q, double J, double dt, double cutoff, int maxm)
   e->slots(8);
   return e;
 }
+// fast != 0: every step runs on the one-wave padded chain (fast_chain.hpp) when
+// its plan builds; returns null if requested and unavailable
+void* emu_new_ex(int L, int p, int Q, double J, double dt, double cutoff, int maxm, int fast) {
+  auto* e = static_cast<Emu*>(emu_new(L, p, Q, J, dt, cutoff, maxm));
+  if (!e || !fast) return e;
+  ocg_host::FastPlanBuild fb = ocg_host::build_fast_plan(e->P, e->md);
+  if (!fb.why_not.empty()) {
+    std::fprintf(stderr, "fast plan: %s\n", fb.why_not.c_str());
+    delete e;
+    return nullptr;
+  }
+  e->fplan = fb.plan;
+  const int off = (e->lds + 255) & ~255;
+  e->P.fplan = e->fplan.data();
+  e->P.fast_off = off;
+  e->lds = off + ocg_host::fast_lds_bytes(e->fplan, e->P);
+  e->P.lds_bytes = e->lds;
+  return e;
+}
 void emu_free(void* h) { delete static_cast<Emu*>(h); }
 int emu_lds_bytes(void* h) { return static_cast<Emu*>(h)->lds; }
 
@@ -163,7 +185,7 @@ void emu_hessian(void* h, const int* dt_, const double* tgt, const int* di, cons
   OcgParams P = e.P;
   const int psi = 6, xi = 6 + N, xih = 6 + 2 * N;
   launch(e, 2, [&](char* smem) {
-    ocg::body_trajectory<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, u, N, 3, e.stats);
+    ocg::body_trajectory<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, u, N, 3, e.stats, 0);
   });
   std::vector<int> xs(N), ys(N);
   std::vector<ocg::zc> r(N);
@@ -232,12 +254,12 @@ void emu_hessian_fused(void* h, const int* dt_, const double* tgt, const int* di
   std::vector<ocg::zc> rsx(size_t(total) * P.cap, ocg::c2(0, 0));
   ocg::Pool rs{rsd.data(), rsx.data()};
   std::vector<double> rn(nrows, 0.0);
-  std::vector<int> flags(2 * N, 0);
+  std::vector<int> flags(2 * N + 3, 0);
   int err = 0;
   const int nxw = N < 8 ? N : 8;
   launch(e, 2 + nxw + nrows, [&](char* smem) {
     ocg::body_pipeline<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, xih, u, N, rows.data(),
-                           nrows, rb.data(), rs, rn.data(), flags.data(), 1, &err, nxw, e.stats);
+                           nrows, rb.data(), rs, rn.data(), flags.data(), 1, &err, nxw, e.stats, 1, 0);
   });
   std::vector<int> xs(N), ys(N);
   std::vector<ocg::zc> pc(N + 1);
@@ -253,7 +275,7 @@ void emu_hessian_fused(void* h, const int* dt_, const double* tgt, const int* di
   std::memset(H, 0, sizeof(double) * N * N);
   launch(e, total, [&](char* smem) {
     ocg::body_row_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), xih, rows.data(), nrows, rb.data(), rs,
-                               rn.data(), pc.data(), pc.data() + N, N, H, e.stats + 9);
+                               rn.data(), pc.data(), pc.data() + N, N, H, e.stats + 9, 1, 0);
   });
   for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
   F[0] = pc[N].x;
@@ -310,7 +332,7 @@ extern "C" int emu_decompose(void* h, int R, int C, const double* M, int dir, do
     c.sync();
     for (int i = c.tid; i < R * C; i += NT) c.TH[i] = ocg::c2(M[2 * i], M[2 * i + 1]);
     c.sync();
-    c.decompose(dir, cutoff, 1 << 30, false, bound.data());
+    c.decompose(dir, cutoff, 1 << 30, false, (LDS const int*)bound.data());
     if (c.tid == 0) {
       kept = c.KEPT[0];
       for (int i = 0; i < R * kept; ++i) { ocg::zc z = c.X[i]; X[2 * i] = z.x; X[2 * i + 1] = z.y; }
@@ -343,7 +365,7 @@ extern "C" void emu_decompose_multi(void* h, int nb, const int* Rs, const int* C
     tot = c.THO[P.Q1];
     for (int i = c.tid; i < tot; i += NT) c.TH[i] = ocg::c2(M[2 * i], M[2 * i + 1]);
     c.sync();
-    c.decompose(dir, cutoff, 1 << 30, false, bound.data());
+    c.decompose(dir, cutoff, 1 << 30, false, (LDS const int*)bound.data());
     if (c.tid == 0) {
       for (int q = 0; q < nb; ++q) kept[q] = c.KEPT[q];
       for (int i = 0; i < c.XOFF[P.Q1]; ++i) { ocg::zc z = c.X[i]; X[2 * i] = z.x; X[2 * i + 1] = z.y; }

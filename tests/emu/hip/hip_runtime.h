@@ -84,12 +84,16 @@ inline long long __double_as_longlong(double v) { long long r; __builtin_memcpy(
 inline double __longlong_as_double(long long v) { double r; __builtin_memcpy(&r, &v, 8); return r; }
 inline int emu_readlane(int v, int l) { return emu_xchg(v, l); }
 inline float emu_rcpf(float x) { return 1.0f / x; }
-// DPP move: row_shr:n (0x111..0x11f), row_bcast:15 (0x142), row_bcast:31 (0x143);
+// DPP move: quad_perm (0x00-0xff), row_shr:n (0x111..0x11f), row_mirror (0x140),
+// row_half_mirror (0x141), row_bcast:15 (0x142), row_bcast:31 (0x143);
 // disabled rows and lanes without a source return `old`
 inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int, bool) {
   const int l = threadIdx.x & 63, row = l >> 4;
   int s = -1;
-  if (ctrl > 0x110 && ctrl < 0x120) { int n = ctrl - 0x110; if ((l & 15) >= n) s = l - n; }
+  if (ctrl >= 0 && ctrl <= 0xff) s = (l & ~3) | ((ctrl >> (2 * (l & 3))) & 3);
+  else if (ctrl > 0x110 && ctrl < 0x120) { int n = ctrl - 0x110; if ((l & 15) >= n) s = l - n; }
+  else if (ctrl == 0x140) s = (l & ~15) | (15 - (l & 15));
+  else if (ctrl == 0x141) s = (l & ~7) | (7 - (l & 7));
   else if (ctrl == 0x142) { if (row >= 1) s = row * 16 - 1; }
   else if (ctrl == 0x143) { if (row >= 2) s = 31; }
   int v = emu_xchg(src, s < 0 ? l : s);
@@ -98,8 +102,14 @@ inline int emu_update_dpp(int old, int src, int ctrl, int row_mask, int, bool) {
 }
 #define __HIP_MEMORY_SCOPE_AGENT 0
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
+#define OCG_EMU 1
 #define __hip_atomic_fetch_add(p, v, o, sc) __atomic_fetch_add((p), (v), __ATOMIC_SEQ_CST)
-#define __hip_atomic_store(p, v, o, sc) __atomic_store_n((p), (v), __ATOMIC_SEQ_CST)
+template <class T, class U>
+inline void emu_atomic_store(T* p, U v) {
+  T t = T(v);
+  __atomic_store(p, &t, __ATOMIC_SEQ_CST);
+}
+#define __hip_atomic_store(p, v, o, sc) emu_atomic_store((p), (v))
 #define __hip_atomic_load(p, o, sc) __atomic_load_n((p), __ATOMIC_SEQ_CST)
 #define __builtin_amdgcn_s_sleep(x) ((void)0)
 inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
@@ -110,5 +120,21 @@ inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 #define __builtin_amdgcn_wave_barrier() emu_wbar->arrive_and_wait()
 inline int emu_bpermute(int addr, int v) { return emu_xchg(v, (addr >> 2) & 63); }
 #define __builtin_amdgcn_ds_bpermute(a, v) emu_bpermute((a), (v))
+// ds_permute: lane l pushes v to lane addr/4; a lane nobody writes reads 0
+// (the last writer wins, as the hardware's highest lane)
+inline int emu_permute(int addr, int v) {
+  const unsigned w = threadIdx.x & ~63u;
+  const int l = threadIdx.x & 63;
+  emu_xbuf[threadIdx.x] = (uint64_t(uint32_t((addr >> 2) & 63)) << 32) | uint32_t(v);
+  emu_wbar->arrive_and_wait();
+  int r = 0;
+  for (int i = 0; i < 64; ++i)
+    if (int(emu_xbuf[w + i] >> 32) == l) r = int(uint32_t(emu_xbuf[w + i]));
+  emu_wbar->arrive_and_wait();
+  return r;
+}
+#define __builtin_amdgcn_ds_permute(a, v) emu_permute((a), (v))
+inline int __ffsll(long long m) { return __builtin_ffsll(m); }
+extern thread_local emu_dim3 gridDim;
 inline double emu_rsq(double x) { return 1.0 / std::sqrt(x); }
 #define __builtin_amdgcn_rsq(x) emu_rsq(x)

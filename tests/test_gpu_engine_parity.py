@@ -202,16 +202,21 @@ def test_fused_equals_unfused_bitwise(states):
 
 
 def _with_plans(flag, fn):
+    """the general chain (OCG_NO_FAST=1: plans belong to it; the one-wave padded
+    chain that steps config-1-sized chains by default has fixed layouts) with
+    decomposition plans on or off"""
     import os
-    old = os.environ.get("OCG_NO_PLANS")
+    old = {k: os.environ.get(k) for k in ("OCG_NO_PLANS", "OCG_NO_FAST")}
     os.environ["OCG_NO_PLANS"] = "0" if flag else "1"
+    os.environ["OCG_NO_FAST"] = "1"
     try:
         return fn()
     finally:
-        if old is None:
-            del os.environ["OCG_NO_PLANS"]
-        else:
-            os.environ["OCG_NO_PLANS"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.mark.parametrize("L,p,N,J,Ui,Uf,cut", [(5, 5, 5, 1.0, 2.5, 50.0, 1e-8), (5, 6, 5, 1.0, 2.0, 12.0, 1e-4),
@@ -272,6 +277,11 @@ def test_maxm_binding_vs_oracle(states, maxm):
     Ho = oc.hessian(u, 4)
     assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
     assert np.abs(0.01 * (divT * F * 1j).real - oc.gradient(u)).max() < 1e-6
+    # the default one-wave padded chain with Maxm binding: the same numbers to rounding
+    Hf, df, Ff = run()
+    assert np.abs(Hf - Ho).max() <= 1e-6 * np.abs(Ho).max()
+    assert np.abs(Hf - H).max() <= 1e-10 * np.abs(H).max()
+    assert np.abs(0.01 * (df * Ff * 1j).real - oc.gradient(u)).max() < 1e-6
 
 
 def _with_env(name, value, fn):
