@@ -6,7 +6,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "libocmps_emu.so")
+LIB = os.environ.get("EMU_LIB") or os.path.join(HERE, "build", "libocmps_emu.so")
 dp = C.POINTER(C.c_double)
 ip = C.POINTER(C.c_int)
 _lib = None

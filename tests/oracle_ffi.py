@@ -15,6 +15,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "build", "libocmps_oracle.so")
+# ORC_LIB: another build of the oracle (the sanitizer builds of tests/test_sanitizers.py)
+_ALT = os.environ.get("ORC_LIB")
 
 _lib = None
 
@@ -27,9 +29,12 @@ def lib():
     if _lib is None:
         src_mtime = max(os.path.getmtime(os.path.join(ORACLE_DIR, f))
                         for f in ("tdmrg_oracle.hpp", "oracle_capi.cpp", "Makefile"))
-        if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < src_mtime:
-            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
-        L = C.CDLL(LIB_PATH)
+        if _ALT:
+            L = C.CDLL(_ALT)
+        else:
+            if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < src_mtime:
+                subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+            L = C.CDLL(LIB_PATH)
         L.orc_new.restype = C.c_void_p
         L.orc_new.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int]
         L.orc_free.argtypes = [C.c_void_p]

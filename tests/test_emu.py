@@ -52,7 +52,7 @@ def test_emulated_fast_pipeline(E):
     Lx, px, Qx, J, dt, cut, maxm = 5, 5, 5, 1.0, 0.01, 1e-8, 80
     di, xi = _gs(Lx, px, Qx, J, 2.5)
     dtg, xtg = _gs(Lx, px, Qx, J, 50.0)
-    N = 7
+    N = 5
     u = np.random.default_rng(3).uniform(2.0, 10.0, N)
     Hf, dvf, Ff = E.Emu(Lx, px, Qx, J, dt, cut, maxm, True).hessian_fused(dtg, xtg, di, xi, u)
     Hg, dvg, Fg = E.Emu(Lx, px, Qx, J, dt, cut, maxm, False).hessian_fused(dtg, xtg, di, xi, u)
