@@ -65,10 +65,13 @@ def parse_args(argv=None):
                     help="weak: every rank its own getHessian; strong: one getHessian's rows over the ranks "
                          "(default: weak for config 1, strong for c4rows / c5rows)")
     ap.add_argument("--group-m", type=int, default=40, help="GROUP basis size of the c4rows workload (0: GRAPE)")
-    ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c4rows", "c5rows"], default="hessian")
+    ap.add_argument("--workload", choices=["hessian", "gradient", "c4grad", "c5grad", "c4rows", "c5rows"], default="hessian")
     ap.add_argument("--c4-nt", type=int, default=33)
     ap.add_argument("--c5-nt", type=int, default=17)
     ap.add_argument("--c5-warm", type=int, default=230)
+    ap.add_argument("--last-rows", type=int, default=0,
+                    help="c4rows / c5rows: only the last R interior rows of H (R >= 1; with --c4-nt 801 / --c5-nt "
+                         "1001 the full horizon, where config 5 selects the trajectory checkpointing by itself)")
     ap.add_argument("--state-cache", default="",
                     help="c4/c5 workloads: npz of psi_init and psi_target, loaded when it exists, else written after "
                          "they are prepared (so a profiled command holds only getHessian launches)")
@@ -228,7 +231,7 @@ def slice_blocks(args):
 
 
 def run(args, blocks=None):
-    if args.workload in ("c4grad", "c4rows", "c5rows"):
+    if args.workload in ("c4grad", "c5grad", "c4rows", "c5rows"):
         return bench_c4(args)
 
     import torch
@@ -583,8 +586,11 @@ def bench_c4(args):
       controls U(2,10), psi_init = the Mott state |1..1> evolved --c5-warm steps
       at U=2.5 on each rank's device (untimed; the bonds saturate at 512 after
       ~220 steps).
-    c4grad: one getAnalyticGradient over the full horizon (N_t=801) per rank
-      (the gradient's time recursion does not shard: replicas).
+    c4grad / c5grad: one getAnalyticGradient over the full horizon (config 4:
+      N_t=801, config 5: N_t=1001) per rank (the gradient's time recursion does
+      not shard: replicas).
+    --last-rows R: the rows N_t-1-R .. N_t-2 only (the cheapest rows of a full
+      horizon: each needs psi_i, xi_i and xiH_i of the whole trajectory).
 
     --mode strong (default for c4rows/c5rows): one Hessian's rows over all
     ranks; --mode weak: every rank a whole Hessian of its own control."""
@@ -594,8 +600,8 @@ def bench_c4(args):
     from optimalcontrolmps_amd.native import MPS, Engine
     rank, world, local, dist, backend = init_dist(args)
     cdev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
-    c5 = args.workload == "c5rows"
-    grad = args.workload == "c4grad"
+    c5 = args.workload in ("c5rows", "c5grad")
+    grad = args.workload in ("c4grad", "c5grad")
     strong = (args.mode or ("weak" if grad else "strong")) == "strong" and not grad
     c = C5 if c5 else C4
     L, p, Q, dt = c["L"], c["p"], c["npart"], c["tstep"]
@@ -654,6 +660,12 @@ def bench_c4(args):
     reduce = torch_reduce(dist, cdev, Nt) if (world > 1 and strong) else None
     project = (lambda Hu: eng.convert_hessian(Hu, basis.V)) if basis is not None else None
 
+    R = args.last_rows if (args.last_rows and not grad) else Nt - 2
+    first = Nt - 1 - R   # the first row of the computed set
+
+    def rows_of(uu, rows):
+        return eng.hessian(uu, [r for r in rows if r >= first])
+
     def one(s):
         if grad:
             if KM > 1:   # K controls: one batch of 2K chains + batched divT / F
@@ -666,7 +678,7 @@ def bench_c4(args):
             F = eng.overlap_factor()
             return dt * (divT * F * 1j).real
         u = control(s)   # GROUP: convertControl (src/ControlBasis.cpp:49-67), host
-        H, divT, F, _ = sharded_hessian(lambda uu, rows: eng.hessian(uu, rows), u, rank if strong else 0,
+        H, divT, F, _ = sharded_hessian(rows_of, u, rank if strong else 0,
                                         world if strong else 1, reduce, gamma=gamma, tstep=dt, project=project)
         return H
 
@@ -705,7 +717,8 @@ def bench_c4(args):
         eng.propagate(control(nsteps_all), 1)
         t_sc = time.perf_counter() - t_sc
     steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
-    row_steps = (Nt - 2) * (Nt - 3) // 2
+    row_steps = R * (R - 1) // 2   # row i steps from i to N_t-2
+    paths = eng.stats(8)
     reps = 1 if strong else world   # independent Hessians / gradients per step
     sweep = args.steps * (steps_traj * (world if (strong or grad) else reps) + (0 if grad else row_steps * reps))
     gemm_ms = gm["ms"] / max(1, gm["launches"])
@@ -717,7 +730,7 @@ def bench_c4(args):
             "metric": ("getAnalyticGradient/sec (psi || xi + divT)" if grad else "Hessian-rows/sec (getHessian)")
                       + (", config 5 chain L=50 Npart=50 d=8 chi=512 tstep=0.01" if c5 else
                          ", config 4 chain L=20 Npart=20 d=6 chi=256 tstep=0.005"),
-            "value": (args.steps * KM * world if grad else args.steps * (Nt - 2) * reps) / elapsed,
+            "value": (args.steps * KM * world if grad else args.steps * R * reps) / elapsed,
             "unit": "gradients/s" if grad else "rows/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
@@ -730,11 +743,14 @@ def bench_c4(args):
                                         "saturated chi=256 warm state (|1..1> evolved 400 steps at U=2.5)")
                      + "; psi_target = psi_init evolved 2 steps at U=6 (SURVEY's |1..1> target has ~1e-10 overlap "
                        "with psi_t, which leaves every derivative at rounding level)"),
-            "config": {"workload": (f"config 4 chain, getAnalyticGradient over N_t={Nt} (T=4)" if grad else
+            "config": {"workload": (f"config {5 if c5 else 4} chain, getAnalyticGradient over N_t={Nt} "
+                                    f"(T={c['T']:g})" if grad else
                                     f"config {5 if c5 else 4} chain, getHessian"
                                     + (f" GROUP M={M} (convertControl, regularisation gamma={gamma}, "
                                        f"convertHessian on the device)" if M else " GRAPE")
-                                    + f" over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)"),
+                                    + (f" over the full horizon N_t={Nt}, the last {R} rows ({row_steps} row-steps)"
+                                       if R < Nt - 2 else
+                                       f" over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)")),
                        "engine": "HBM-resident (hbm.hip)", "parallelism": par},
             "sweep_steps_per_sec": sweep / elapsed,
             "single_chain_steps_per_sec": (Nt - 1) / t_sc if t_sc else None,
@@ -751,6 +767,10 @@ def bench_c4(args):
                                        limiter="the per-sector Hermitian eigensolver (k_heev_*) sets the step time; "
                                                "k_gemm launches are small (tasks of m, n ~ 16-60) and latency-bound"),
         }
+        if not grad:
+            res["hessian_path"] = {"pipelined": paths["launches"], "pipeline_fallbacks": paths["sweep_steps"],
+                                   "checkpointed": int(paths["alg_flops"]),
+                                   "checkpoint_segment": int(paths["alg_bytes"]) or None}
         res["env"] = run_env()
         if world == 1 and not args.no_cpu_baseline and not grad and not args.profiled:
             res["cpu_baseline"] = (cpu_baseline_c5(ini, Nt, args.cpu_threads) if c5 else

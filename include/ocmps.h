@@ -220,8 +220,9 @@ int ocg_denmat_decomp(ocg_ctx* ctx, int nm, const int* rows, const int* cols, co
  * zeros on the LDS engine), 8 the HBM engine's getHessian path counters
  * (*launches = pipelined getHessians completed, *sweep_steps = two-phase
  * retries after a pipeline that failed with OCG_ENOMEM; never with
- * OCG_HBM_PIPE=1, which makes any pipeline failure the call's status).  Sums
- * since the last reset. */
+ * OCG_HBM_PIPE=1, which makes any pipeline failure the call's status),
+ * *alg_flops = trajectory-checkpointed getHessians completed, *alg_bytes = the
+ * segment length of the last one).  Sums since the last reset. */
 int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
                      double* alg_flops, long* sweep_steps);
 int ocg_reset_stats(ocg_ctx* ctx);

@@ -26,7 +26,7 @@ enum {
   kHSite,        // site element ranges [k] = first padded element of site k (k = 0..L+1)
   kHSiteN,       // per padded element of site 1: its physical index n (phases)
   kHNops,        // step operations
-  kHZMps,        // complex offsets in the fast LDS region: MPS,
+  kHZMps,        // complex offsets in the fast LDS region: MPS (its zero slot at index kHNp),
   kHZTh,         //   matricisation / Θ,
   kHZTg,         //   gated Θ,
   kHZW,          //   eigenvector blocks (4 groups x 16),
@@ -36,6 +36,8 @@ enum {
   kHZTot,        // complex elements of the region
   kHNint,        // ints of the plan image
   kHCentre,      // orthogonality centre after a step without the closing move
+  kHThZ,         // the zero slot of the Θ / gated-Θ buffers (complex index; never written)
+  kHXsZ,         // the zero slot of the factor scratch
   kHOps,         // kMaxOps op offsets follow
   kHdrInts = kHOps + kMaxOps
 };
@@ -54,6 +56,7 @@ enum {
   kOhSecQ,           // sector s -> q of the rewritten bond (ints)
   kOhF, kOhNf,       // factor elements: int4 (see fast_plan.hpp)
   kOhS, kOhNs,       // gauge product elements: int4 {x1 | x2 << 16, len | s2 << 16, dest, 0}
+  kOhDot,            // longest Gram / order-1 dot product of the decomposition
   kOhGrp = 24,       // 4 groups x 8 ints: s, n, side, tho, R, C, eoff, 0 (16-byte aligned)
   kOpHdr = kOhGrp + 32
 };

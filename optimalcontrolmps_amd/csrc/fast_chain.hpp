@@ -40,14 +40,16 @@ struct FastChain {
   const int lane;
   const bool act;  // wave 0
   lzp MP, TH, TG, WB, XS, GT, PH;
-  LDS double *LAM, *SIG;
+  LDS double *LAM, *SIG, *SIGI;
   LDS int *DIM, *BOF, *KQ, *WIDX, *PL;
   int np, nblk, o_blk, o_ls, o_site, o_siten, nops, centre_open;
+  int thz, xsz;  // zero slots of TH / TG and XS (MP's is np)
   double ph_u = __builtin_nan("");
   int ph_dir = -1;
   // dims_epoch counts bond-dimension changes (block offsets are recomputed
   // only after one)
   int dims_epoch = 0, bof_epoch = -1;
+  int trace_op = -1;  // diagnostics: the step operation being run
   // algorithmic-traffic model (the general chain's accounting), per lane
   double m_bytes = 0, m_flops = 0;
   // diagnostic build (-DOCG_PROFILE): shader-clock cycles per phase into the
@@ -67,6 +69,16 @@ struct FastChain {
     (void)cat;
 #endif
   }
+  // diagnostic build: event counts into PROF slots 20..22, 30 (jacobi sweeps,
+  // calls, decompositions, rounds)
+  __device__ __forceinline__ void cnt(int slot, double v) {
+#ifdef OCG_PROFILE
+    if (threadIdx.x == 0 && PROF) PROF[slot] += v;
+#else
+    (void)slot;
+    (void)v;
+#endif
+  }
 
   // base: the fast region of the dynamic LDS (fast_lds_bytes of the plan)
   __device__ OCG_INLINE FastChain(const OcgParams& P_, char* base, const int* gplan, LDS double* prof = nullptr)
@@ -76,12 +88,13 @@ struct FastChain {
     // the header is read from global memory (uniform scalar loads)
     np = gplan[kHNp]; nblk = gplan[kHNblk]; o_blk = gplan[kHBlk]; o_ls = gplan[kHLs]; o_site = gplan[kHSite];
     o_siten = gplan[kHSiteN]; nops = gplan[kHNops]; centre_open = gplan[kHCentre];
+    thz = gplan[kHThZ]; xsz = gplan[kHXsZ];
     lzp cb{(LDS double*)base};
     MP = cb + gplan[kHZMps]; TH = cb + gplan[kHZTh]; TG = cb + gplan[kHZTg]; WB = cb + gplan[kHZW];
     XS = cb + gplan[kHZX]; GT = cb + gplan[kHZGt]; PH = cb + gplan[kHZPh];
     LDS double* db = (cb + gplan[kHZTot]).p;
-    LAM = db; SIG = db + 64;  // then 8 spare doubles
-    LDS int* ib = (LDS int*)(db + 136);
+    LAM = db; SIG = db + 64; SIGI = db + 128;  // then 8 spare doubles
+    LDS int* ib = (LDS int*)(db + 200);
     auto al = [](int x) { return (x + 3) & ~3; };  // 16-byte aligned int arrays
     DIM = ib; ib += al(P.nsq);
     BOF = ib; ib += al(nblk);
@@ -96,12 +109,21 @@ struct FastChain {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   __device__ __forceinline__ static i4 ld4(const LDS int* p) { return *(const LDS i4*)p; }
+  // op-header fields are wave-uniform: scalar registers, uniform branches
+  __device__ __forceinline__ static int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
   // plan image and gate tables into LDS (once per launch)
   __device__ OCG_INLINE void init(const int* gplan, const zc* gf, const zc* gb) {
     if (!act) return;
     const int ni = gplan[fastp::kHNint];
     for (int i = lane; i < ni; i += 64) PL[i] = gplan[i];
     for (int i = lane; i < P.gtotal; i += 64) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
+    if (lane == 0) {
+      WB[64] = c2(1.0, 0.0);  // the eigenvector of every order-1 sector
+      MP[np] = c2(0.0, 0.0);  // zero slots
+      TH[thz] = c2(0.0, 0.0);
+      TG[thz] = c2(0.0, 0.0);
+      XS[xsz] = c2(0.0, 0.0);
+    }
     wsync();
   }
   __device__ __forceinline__ int dim(int b, int q) const { return (q < 0 || q > P.Q) ? 0 : DIM[b * P.Q1 + q]; }
@@ -197,19 +219,32 @@ struct FastChain {
   // 16 (2 (|A_i1| + |A_i2|) + gate) bytes, 8 (R C m + R C p + n^2 max(R, C) +
   // 2 R C m) flops per middle sector (Chain::build_theta's accounting)
   __device__ OCG_INLINE void model_gate(int i1) {
-    const int p = P.p, Q1 = P.Q1, q = lane;
-    double fl = 0.0, by = 0.0;
-    if (q < Q1) {
-      int R = 0, C = 0, u = 0;
-      const int m = dim(i1, q), dl = dim(i1 - 1, q);
+    // all 3 p bond dims of the three bonds in one wave of loads (clamped
+    // addresses, out-of-range sectors selected to 0)
+    const int p = P.p, Q = P.Q, Q1 = P.Q1, q = lane < Q1 ? lane : 0;
+    const LDS int* d0 = DIM + (i1 - 1) * Q1;
+    const LDS int* d1 = DIM + i1 * Q1;
+    const LDS int* d2 = DIM + (i1 + 1) * Q1;
+    int l[6], a[6], r[6];
 #pragma unroll
-      for (int n = 0; n < 6; ++n) {
-        if (n < p) {
-          R += dim(i1 - 1, q - n);
-          C += dim(i1 + 1, q + n);
-          u += dl * dim(i1, q + n) + m * dim(i1 + 1, q + n);
-        }
-      }
+    for (int n = 0; n < 6; ++n) {
+      const int qm = q - n, qp = q + n;
+      const bool okm = n < p && qm >= 0, okp = n < p && qp <= Q;
+      const int lm = d0[okm ? qm : 0], ap = d1[okp ? qp : 0], rp = d2[okp ? qp : 0];
+      l[n] = okm ? lm : 0;
+      a[n] = okp ? ap : 0;
+      r[n] = okp ? rp : 0;
+    }
+    int R = 0, C = 0, u = 0;
+    const int m = a[0], dl = l[0];
+#pragma unroll
+    for (int n = 0; n < 6; ++n) {
+      R += l[n];
+      C += r[n];
+      u += dl * a[n] + m * r[n];
+    }
+    double fl = 0.0, by = 0.0;
+    if (lane < Q1) {
       if (R == 0 || C == 0) { R = 0; C = 0; }
       const double Rd = R, Cd = C, nn = R < C ? R : C;
       fl = 8.0 * (Rd * Cd * m + Rd * Cd * p + nn * nn * (R > C ? Rd : Cd) + 2.0 * Rd * Cd * m);
@@ -224,8 +259,8 @@ struct FastChain {
   __device__ OCG_INLINE void theta(const LDS int* oh) {
     using namespace fastp;
     pf(0);
-    const int nth = oh[kOhNth];
-    const LDS int* md = PL + oh[kOhMat];
+    const int nth = uni(oh[kOhNth]);
+    const LDS int* md = PL + uni(oh[kOhMat]);
     int d0[kItTh], d1[kItTh];
 #pragma unroll
     for (int it = 0; it < kItTh; ++it) {
@@ -242,8 +277,8 @@ struct FastChain {
 #pragma unroll
       for (int b = 0; b < kMaxDm; ++b) {
         const int bb = b < dmc ? b : dmc;
-        const zc a = MP[x1 + bb], v = MP[x2 + bb * drc];
-        if (b < dm) cacc(acc, a, v);
+        const zc a = MP[b < dm ? x1 + b : np], v = MP[x2 + bb * drc];  // beyond dm: the zero slot
+        cacc(acc, a, v);
       }
       if (e < nth) TH[e] = acc;
     }
@@ -251,11 +286,26 @@ struct FastChain {
   }
   // pre-phase -> hopping gate (per Δ = n1 + n2 block) -> post-phase (Chain::apply_gate).
   // PH holds UF[p], UT[p], then the pair products UF[n1] UF[n2] and UT[a1] UT[a2] (p^2 each)
+  // PRE: 0 none, 1 the pair UF[n1] UF[n2], 2 UF[n2] alone; POST: 0 none, 1 the
+  // pair UT[a1] UT[a2], 2 UT[a2] alone (compile-time: no per-element selects)
   __device__ OCG_INLINE void gate(const LDS int* oh, int forward) {
     using namespace fastp;
     pf(1);
-    const int p = P.p, nth = oh[kOhNth], mode = oh[kOhMode], lonely = oh[kOhLonely];
-    const LDS int* gd = PL + oh[kOhGate];
+    const int mode = uni(oh[kOhMode]), lonely = uni(oh[kOhLonely]);
+    if (mode == 0) {
+      if (lonely & 1) gate_body<1, 2>(oh, forward);
+      else gate_body<1, 0>(oh, forward);
+    } else {
+      if (lonely & 2) gate_body<2, 1>(oh, forward);
+      else gate_body<0, 1>(oh, forward);
+    }
+    wsync();
+  }
+  template <int PRE, int POST>
+  __device__ OCG_INLINE void gate_body(const LDS int* oh, int forward) {
+    using namespace fastp;
+    const int p = P.p, nth = uni(oh[kOhNth]);
+    const LDS int* gd = PL + uni(oh[kOhGate]);
     lzp g0 = GT + (forward ? 0 : P.gtotal);
     lzp UF = PH, UT = PH + p, UFF = PH + 2 * p, UTT = PH + 2 * p + p * p;
     i4 d[kItTh];
@@ -276,24 +326,23 @@ struct FastChain {
         const int xx = x < sz ? x : sz - 1;
         const int n1 = lo + xx, n2 = D - n1;
         const int ad = (unsigned(d[it][1 + (x >> 1)]) >> (16 * (x & 1))) & 0xffff;
-        zc z = TH[x < sz ? ad : 0];
-        const zc ph = mode == 0 ? zc(UFF[n1 * p + n2]) : zc(UF[n2]);
-        if (mode == 0 || (lonely & 2)) z = cmul(z, ph);
+        zc z = TH[x < sz ? ad : thz];  // beyond sz: the zero slot
+        if (PRE == 1) z = cmul(z, UFF[n1 * p + n2]);
+        if (PRE == 2) z = cmul(z, UF[n2]);
         const zc gx = g[xx];
-        if (x < sz) cacc(acc, gx, z);
+        cacc(acc, gx, z);
       }
-      const zc po = mode == 1 ? zc(UTT[a1 * p + a2]) : zc(UT[a2]);
-      if (mode == 1 || (lonely & 1)) acc = cmul(acc, po);
+      if (POST == 1) acc = cmul(acc, UTT[a1 * p + a2]);
+      if (POST == 2) acc = cmul(acc, UT[a2]);
       if (e < nth) TG[e] = acc;
     }
-    wsync();
   }
   // single-site matricisation (gauge moves): M[e] = A[src[e]]
   __device__ OCG_INLINE void matcopy(const LDS int* oh) {
     using namespace fastp;
     pf(7);
-    const int nth = oh[kOhNth];
-    const LDS int* src = PL + oh[kOhMat];
+    const int nth = uni(oh[kOhNth]);
+    const LDS int* src = PL + uni(oh[kOhMat]);
     int s[kItTh];
 #pragma unroll
     for (int it = 0; it < kItTh; ++it) {
@@ -318,7 +367,7 @@ struct FastChain {
   __device__ OCG_INLINE void decompose(const LDS int* oh, lzp M, int dir, double cutoff, int maxm, bool normalize) {
     using namespace fastp;
     pf(2);
-    const int nsec = oh[kOhNsec], T = oh[kOhT], maxr = oh[kOhMaxr], no1 = oh[kOhNo1];
+    const int nsec = uni(oh[kOhNsec]), T = uni(oh[kOhT]), maxr = uni(oh[kOhMaxr]), no1 = uni(oh[kOhNo1]);
     // ---- Gram of the Jacobi groups: lane 16 g + 4 i + j holds G[i][j]
     const int g = lane >> 4, i = (lane >> 2) & 3, j = lane & 3, rb = lane & ~15;
     const i4 ga = ld4(oh + kOhGrp + 8 * g), gb = ld4(oh + kOhGrp + 8 * g + 4);
@@ -326,33 +375,31 @@ struct FastChain {
     const int n = used ? ga[1] : 0, side = ga[2], tho = ga[3], R = gb[0], C = gb[1], eoff = gb[2];
     const bool valid = i < n && j < n;
     // order-1 sectors (lanes < no1): the block's one row / column squared norm
-    const i4 o1 = ld4(PL + oh[kOhO1] + 4 * (lane < no1 ? lane : 0));
+    const i4 o1 = ld4(PL + uni(oh[kOhO1]) + 4 * (lane < no1 ? lane : 0));
+    // G[i][j] = sum_c a_c conj(b_c) on either side (cols side: the conjugate of
+    // that sum); the loop is unrolled to the op's longest dot product (header,
+    // uniform), indices beyond a block's length read the zero slot
     zc gv = c2(0.0, 0.0);
     double lam1 = 0.0;
     {
       const int len = used ? (side == 0 ? C : R) : 0, st = side == 0 ? 1 : C;
       const int bi = side == 0 ? tho + (i < n ? i : 0) * C : tho + (i < n ? i : 0);
       const int bj = side == 0 ? tho + (j < n ? j : 0) * C : tho + (j < n ? j : 0);
-      const int lc = len > 0 ? len - 1 : 0;
-      const int len1 = lane < no1 ? o1[1] : 0;
-      const int l1 = len1 > 0 ? len1 - 1 : 0;
-#pragma unroll
-      for (int c = 0; c < kMaxDot; ++c) {
-        const int cc = c < lc ? c : lc;
-        const zc a = M[used ? bi + cc * st : 0], b = M[used ? bj + cc * st : 0];
-        const int c1 = c < l1 ? c : l1;
-        const zc z1 = M[len1 > 0 ? o1[0] + c1 * o1[2] : 0];
-        if (c < len) {
-          if (side == 0) cacc(gv, a, cconj(b));
-          else cjacc(gv, a, b);
-        }
-        if (c < len1) lam1 += cabs2(z1);
-      }
+      const int len1 = lane < no1 ? o1[1] : 0, b1 = o1[0], s1 = o1[2];
+      const int dot = uni(oh[kOhDot]);
+      if (dot <= 4) gram_dots<4>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
+      else if (dot <= 8) gram_dots<8>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
+      else gram_dots<kMaxDot>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
+      if (side == 1) gv.y = -gv.y;
     }
     if (!valid) gv = c2(0.0, 0.0);
     zc w = c2(i == j ? 1.0 : 0.0, 0.0);
+#ifdef OCG_FAST_TRACE
+    if (trace_op == 1 && valid) printf("[gram] grp %d side %d n %d R %d C %d (%d,%d) %.3e %.3e\n", g, side, n, R, C, i, j, gv.x, gv.y);
+#endif
     pf(3);
     if (maxr > 0) jacobi(gv, w, valid, i, j, rb, n, maxr);
+    cnt(22, 1.0);
     pf(4);
     // eigenvectors and eigenvalues (clamped at 0) to LDS
     if (used) WB[16 * g + 4 * i + j] = w;
@@ -361,16 +408,19 @@ struct FastChain {
     wsync();
     // ---- truncation (Chain::decompose, one-wave form): eigen slot e = lane
     const bool ae = lane < T;
-    const i4 eq = ld4(PL + oh[kOhEq] + 4 * (ae ? lane : 0));
+    const i4 eq = ld4(PL + uni(oh[kOhEq]) + 4 * (ae ? lane : 0));
     const double lam = ae ? LAM[lane] : 0.0;
     const int s_e = eq[0], i_e = eq[1], eo_e = eq[2], n_e = eq[3] & 255, bound = unsigned(eq[3]) >> 8;
     // rank inside the block (descending, ties by index)
+    // (all partner values fetched first; non-short-circuit predicates keep the
+    // compares free of branches, so the four exchanges are in flight together)
+    double lt[kMaxGram];
+#pragma unroll
+    for (int t = 0; t < kMaxGram; ++t) lt[t] = CH::bperm(lam, ((eo_e + t) & 63) << 2);
     int jb = 0;
 #pragma unroll
-    for (int t = 0; t < kMaxGram; ++t) {
-      const double lt = CH::bperm(lam, ((eo_e + t) & 63) << 2);
-      jb += (ae && t < n_e && t != i_e && (lt > lam || (lt == lam && t < i_e))) ? 1 : 0;
-    }
+    for (int t = 0; t < kMaxGram; ++t)
+      jb += (ae & (t < n_e) & (t != i_e) & ((lt[t] > lam) | ((lt[t] == lam) & (t < i_e)))) ? 1 : 0;
     const double total = wsum(lam);
     const double cut = cutoff * total, floor_ = 1e-30 * total;
     bool disc = false;
@@ -379,6 +429,8 @@ struct FastChain {
       const double thr = fmax(cut, floor_);
       const bool small = ae && (lam < thr || lam <= floor_);
       unsigned long long Mk = __ballot(small);
+      pf(18);
+      cnt(17, __popcll(Mk));
       if (Mk) {
         const int nbig = T - __popcll(Mk);
         double S = lam;
@@ -413,10 +465,13 @@ struct FastChain {
       const int m = T - __popcll(__ballot(d2));
       disc = ae && rk >= m;
     }
+    pf(16);
     const bool kept = ae && !disc && jb < bound;
     if (kept) {
+      const double sq = sqrt(lam);
       WIDX[eo_e + jb] = i_e;
-      SIG[eo_e + jb] = sqrt(lam);
+      SIG[eo_e + jb] = sq;
+      SIGI[eo_e + jb] = sq > 0 ? 1.0 / sq : 0.0;  // the factors' 1 / sigma, once per eigenvalue
     }
     const double kw = wsum(kept ? lam : 0.0);
     int kq = 0;
@@ -425,8 +480,8 @@ struct FastChain {
       kq = (lane == s) ? c : kq;
     }
     {
-      const int newb = oh[kOhNewBond];
-      const int q = lane < nsec ? PL[oh[kOhSecQ] + lane] : 0;
+      const int newb = uni(oh[kOhNewBond]);
+      const int q = lane < nsec ? PL[uni(oh[kOhSecQ]) + lane] : 0;
       bool changed = false;
       if (lane < nsec) {
         const int at = newb * P.Q1 + q;
@@ -440,13 +495,32 @@ struct FastChain {
     pf(5);
     // ---- factors (Chain::decompose's materialisation): X rows, Y cols
     const double inv = (normalize && kw > 1e-32) ? 1.0 / sqrt(kw) : 1.0;
-    const int nf = oh[kOhNf];
-    const LDS int* fl = PL + oh[kOhF];
+    const int nf = uni(oh[kOhNf]);
+    const LDS int* fl = PL + uni(oh[kOhF]);
     i4 fd[kItF];
 #pragma unroll
     for (int it = 0; it < kItF; ++it) {
       const int e = lane + 64 * it;
       fd[it] = ld4(fl + 4 * (e < nf ? e : nf - 1));
+    }
+    // operands in two dependent waves of loads, all elements at once: (KQ, WIDX,
+    // SIG, the M terms), then the eigenvector entries W[., wv]; branch-free
+    // (an exact factor is a selected entry of W, a derived one sum_x M W)
+    int kqs[kItF], wvv[kItF];
+    double sg[kItF], isg[kItF];
+    zc mv[kItF][kMaxGram];
+#pragma unroll
+    for (int it = 0; it < kItF; ++it) {
+      const int w0 = fd[it][0], w1 = fd[it][1], w2 = fd[it][2];
+      const int s = (w0 >> 16) & 15, jj = (w0 >> 20) & 15, eo = w2 & 255;
+      const bool exact = (w2 >> 12) & 1;
+      const int mb = w1 & 0xffff, terms = (w1 >> 16) & 31, ms = unsigned(w1) >> 21;
+      kqs[it] = KQ[s];
+      wvv[it] = WIDX[eo + jj];
+      sg[it] = SIG[eo + jj];
+      isg[it] = SIGI[eo + jj];
+#pragma unroll
+      for (int x = 0; x < kMaxGram; ++x) mv[it][x] = M[(exact || x >= terms) ? thz : mb + x * ms];
     }
     zc out[kItF];
     int dst[kItF];
@@ -454,43 +528,58 @@ struct FastChain {
     for (int it = 0; it < kItF; ++it) {
       const int e = lane + 64 * it;
       const int w0 = fd[it][0], w1 = fd[it][1], w2 = fd[it][2], wbse = fd[it][3];
-      const int dest = w0 & 0xffff, s = (w0 >> 16) & 15, jj = (w0 >> 20) & 15;
+      const int dest = w0 & 0xffff, jj = (w0 >> 20) & 15;
       const bool isx = (w0 >> 24) & 1, scr = (w0 >> 25) & 1;
-      const int eo = w2 & 255, ns = (w2 >> 8) & 15;
       const bool exact = (w2 >> 12) & 1;
-      const int kqs = KQ[s], wv = WIDX[eo + jj];
-      const double sig = SIG[eo + jj];
-      const bool live = jj < kqs && e < nf;
-      const int wvc = live ? wv : 0;
-      zc r = c2(0.0, 0.0);
-      if (exact) {
-        const zc wx = ns == 1 ? c2(1.0, 0.0) : zc(WB[w1 + wvc]);
-        r = isx ? wx : cconj(wx);
-        if (isx ? dir == kFromright : dir == kFromleft) r = cscale(r, sig * inv);
-      } else {
-        const int mb = w1 & 0xffff, terms = (w1 >> 16) & 31, ms = unsigned(w1) >> 21;
-        const int tc = terms > 0 ? terms - 1 : 0;
-        zc acc = c2(0.0, 0.0);
+      const int terms = exact ? 1 : (w1 >> 16) & 31;
+      const int tc = terms > 0 ? terms - 1 : 0;
+      const bool live = jj < kqs[it] && e < nf;
+      const int wvc = live ? wvv[it] : 0;
+      const int base = exact ? w1 : wbse;  // an order-1 sector points at the unit slot WB[64]
+      const double cs = isx ? 1.0 : -1.0;  // w (Θ w) or conj(w) (w^H Θ)
+      zc wp[kMaxGram];
 #pragma unroll
-        for (int x = 0; x < kMaxGram; ++x) {
-          const int xx = x < tc ? x : tc;
-          const zc mv = M[mb + xx * ms];
-          const zc wx = ns == 1 ? c2(1.0, 0.0) : zc(WB[(wbse > 0 ? wbse : 0) + 4 * xx + wvc]);
-          if (x < terms) {
-            if (isx) cacc(acc, mv, wx);  // Θ w
-            else cjacc(acc, wx, mv);     // w^H Θ
-          }
-        }
-        const bool orth = isx ? dir == kFromleft : dir == kFromright;  // the orthonormal side divides by sigma
-        r = orth ? (sig > 0 ? cscale(acc, 1.0 / sig) : c2(0.0, 0.0)) : cscale(acc, inv);
+      for (int x = 0; x < kMaxGram; ++x) {
+        const zc t = WB[base + 4 * (x < tc ? x : tc) + wvc];
+        wp[x] = c2(t.x, cs * t.y);
       }
+      zc acc = c2(0.0, 0.0);
+#pragma unroll
+      for (int x = 0; x < kMaxGram; ++x) cacc(acc, mv[it][x], wp[x]);  // beyond terms: the zero slot
+      // exact: the selected entry of W, times sigma / sqrt(kept weight) on the
+      // norm-carrying side; derived: divided by sigma on the orthonormal side
+      const double sig = sg[it];
+      const zc we = wp[0];
+      const bool scl = isx ? dir == kFromright : dir == kFromleft;
+      const bool orth = isx ? dir == kFromleft : dir == kFromright;
+      const double f = exact ? (scl ? sig * inv : 1.0) : (orth ? (sig > 0 ? isg[it] : 0.0) : inv);
+      const zc r = cscale(exact ? we : acc, f);
       out[it] = live ? r : c2(0.0, 0.0);
       dst[it] = e < nf ? (dest | (scr ? 0x10000 : 0)) : -1;
     }
+    pf(23);
 #pragma unroll
     for (int it = 0; it < kItF; ++it)
       if (dst[it] >= 0) ((dst[it] >> 16) ? XS : MP)[dst[it] & 0xffff] = out[it];
     wsync();
+  }
+
+  template <int K>
+  __device__ __forceinline__ void gram_dots(lzp M, int len, int st, int bi, int bj, int len1, int b1, int s1, zc& gv,
+                                            double& lam1) const {
+    zc a[K], b[K], z[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const bool in = c < len, in1 = c < len1;
+      a[c] = M[in ? bi + c * st : thz];
+      b[c] = M[in ? bj + c * st : thz];
+      z[c] = M[in1 ? b1 + c * s1 : thz];
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      cacc(gv, a[c], cconj(b[c]));
+      lam1 += cabs2(z[c]);
+    }
   }
 
   // register Jacobi on up to four Gram blocks of order <= 4 (Chain::jacobi_reg<4>):
@@ -515,7 +604,7 @@ struct FastChain {
       fl[rnd] = (i < j && pi == j ? 1 : 0) | (j < pj ? 2 : 0) | (i < pi ? 4 : 0) | (pj != j ? 8 : 0) |
                 (pi != i ? 16 : 0) | (pi == j ? 32 : 0);
     }
-    int sweep = 0;
+    int sweep = 0, nr = 0;
     bool done = false;
     for (; sweep < 40; ++sweep) {
       bool flag = false;
@@ -528,6 +617,7 @@ struct FastChain {
           done = true;
           break;
         }
+        ++nr;
         zc cs, e;
         double sh;
         CH::jrot_fast(g, di, dj, need, cs, e, sh);
@@ -571,6 +661,12 @@ struct FastChain {
       if (done || __ballot(flag) == 0) break;
     }
     if (sweep == 40 && lane == 0 && P.err) atomicOr(P.err, OCG_ERR_JACOBI);
+    cnt(21, 1.0);
+    cnt(20, double(sweep + 1));
+    cnt(30, double(nr));
+#ifdef OCG_FAST_TRACE  // CPU emulation diagnostics (tests/emu, EXTRA=-DOCG_FAST_TRACE)
+    if (lane == 0) printf("[jacobi] op %d sweeps %d rounds %d\n", trace_op, sweep + 1, nr);
+#endif
   }
 
   // ------------------------------------------------------------- gauge neighbour
@@ -578,8 +674,8 @@ struct FastChain {
   __device__ OCG_INLINE void neighbour(const LDS int* oh) {
     using namespace fastp;
     pf(25);
-    const int ns = oh[kOhNs], kind = oh[kOhKind];
-    const LDS int* sl = PL + oh[kOhS];
+    const int ns = uni(oh[kOhNs]), kind = uni(oh[kOhKind]);
+    const LDS int* sl = PL + uni(oh[kOhS]);
     i4 d[kItS];
 #pragma unroll
     for (int it = 0; it < kItS; ++it) {
@@ -596,9 +692,10 @@ struct FastChain {
 #pragma unroll
       for (int b = 0; b < kMaxDm; ++b) {
         const int bb = b < lc ? b : lc;
-        const zc a = (kind == kOpGaugeR) ? zc(XS[x1 + bb]) : zc(MP[x1 + bb]);
+        const bool in = b < len;  // beyond len: the zero slot of the first operand's buffer
+        const zc a = (kind == kOpGaugeR) ? zc(XS[in ? x1 + b : xsz]) : zc(MP[in ? x1 + b : np]);
         const zc v = (kind == kOpGaugeR) ? zc(MP[x2 + bb * s2]) : zc(XS[x2 + bb * s2]);
-        if (b < len) cacc(acc[it], a, v);
+        cacc(acc[it], a, v);
       }
     }
     wsync();
@@ -644,11 +741,12 @@ struct FastChain {
     for (int o = 0; o < nops; ++o) {
       const LDS int* oh = PL + PL[kHOps + o];
       const i4 h0 = ld4(oh), h1 = ld4(oh + 4);
-      if (h1[1] && !final_gauge) continue;  // closing move
-      const int kind = h0[0], dir = h0[2];
+      if (uni(h1[1]) && !final_gauge) continue;  // closing move
+      const int kind = uni(h0[0]), dir = uni(h0[2]);
+      trace_op = o;
       if (kind == kOpGate) {
         pf(12);
-        model_gate(h0[1]);
+        model_gate(uni(h0[1]));
         theta(oh);
         gate(oh, forward);
         decompose(oh, TG, dir, P.cutoff, P.maxm, true);

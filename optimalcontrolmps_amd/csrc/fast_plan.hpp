@@ -21,6 +21,8 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -235,12 +237,22 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
         grp = ngrp++;
       }
       seco[q] = int(sq.size());
-      secn[q] = n; secside[q] = R[q] <= C[q] ? 0 : 1; secgrp[q] = grp; seceoff[q] = T;
+      // Gram on the smaller side; on a tie, a gauge move takes the side of the
+      // bond it does not rewrite (cols for a right move, rows for a left move):
+      // that bond is already in its Schmidt basis (the previous decomposition of
+      // it diagonalised the same reduced density matrix), so the Gram is
+      // diagonal up to the truncations since and the Jacobi has nothing to do
+      int side = R[q] < C[q] ? 0 : (R[q] > C[q] ? 1 : 0);
+      if (R[q] == C[q] && o.kind == kOpGaugeR) side = 1;
+      secn[q] = n; secside[q] = side; secgrp[q] = grp; seceoff[q] = T;
       sq.push_back(q);
       T += n;
       maxn = std::max(maxn, n);
     }
     const int nsec = int(sq.size());
+    int maxdot = 1;
+    for (int q : sq) maxdot = std::max(maxdot, std::max(R[q], C[q]));
+    setH(kOhDot, maxdot);
     if (nsec > 15) return fail("more than 15 sectors");
     if (T > 64) return fail("more than 64 eigenvalues per decomposition");
     setH(kOhNsec, nsec); setH(kOhT, T); setH(kOhNgrp, ngrp);
@@ -276,7 +288,7 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
     //   w1 = exact: W offset of row idx (grp 16 + 4 idx); derived: M offset of the
     //        first term | terms << 16 | M stride << 21
     //   w2 = eigen offset of s | n << 8 | exact << 12
-    //   w3 = W offset of the group (grp 16; -1 for an order-1 sector: W = 1)
+    //   w3 = W offset of the group (grp 16; 64 for an order-1 sector: the unit slot)
     // X rows of the left factor, Y cols of the right one; every destination is a
     // whole padded site (or scratch block): columns / rows j >= kept get zeros
     std::vector<int> XS_off(Q1, 0), YS_off(Q1, 0);
@@ -286,10 +298,10 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
     auto pushf = [&](int dest, int q, int j, bool isx, bool scratch, int idx) {
       const int s = seco[q], n = secn[q], side = secside[q], g = secgrp[q];
       const bool exact = isx ? side == 0 : side == 1;
-      const int wb = g >= 0 ? 16 * g : -1;
+      const int wb = g >= 0 ? 16 * g : 64;  // order 1: the unit slot WB[64]
       int w1;
       if (exact) {
-        w1 = (wb >= 0 ? wb : 0) + 4 * idx;
+        w1 = wb + (g >= 0 ? 4 * idx : 0);
       } else if (isx) {  // X[idx][j] = sum_c M[idx][c] W[c][w], c < C = n
         w1 = (THO[q] + idx * C[q]) | (n << 16) | (1 << 21);
       } else {  // Y[j][idx] = sum_r conj(W[r][w]) M[r][idx], r < R = n
@@ -382,11 +394,15 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
   I[kHSiteN] = o_siten;
   I[kHNops] = int(ops.size());
   for (size_t i = 0; i < ops.size(); ++i) I[kHOps + int(i)] = op_off[i];
-  I[kHZMps] = take(np);
-  I[kHZTh] = take(thmax);
-  I[kHZTg] = take(thmax);
-  I[kHZW] = take(64);
-  I[kHZX] = take(xsmax);
+  // every operand buffer ends in a zero slot that no phase writes: a clamped
+  // index beyond an element's term count points there instead of a select
+  I[kHZMps] = take(np + 1);
+  I[kHZTh] = take(thmax + 1);
+  I[kHZTg] = take(thmax + 1);
+  I[kHZW] = take(65);  // 4 groups x 16, then the unit slot
+  I[kHZX] = take(xsmax + 1);
+  I[kHThZ] = thmax;
+  I[kHXsZ] = xsmax;
   I[kHZGt] = take(2 * P.gtotal);
   I[kHZPh] = take(2 * p + 2 * p * p);  // UF, UT, UF UF, UT UT
   I[kHZTot] = zc_off;
@@ -394,13 +410,21 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
   pad();
   I[kHNint] = int(I.size());
   if (I.size() > 65535) return fail("plan too large");
+  if (std::getenv("OCG_FAST_DUMP")) {  // diagnostic: the step's operations
+    for (size_t i = 0; i < ops.size(); ++i) {
+      const int* h = &I[op_off[i]];
+      std::fprintf(stderr, "[fast plan] op %zu kind %d k %d nth %d nsec %d T %d ngrp %d maxr %d dot %d no1 %d nf %d ns %d\n",
+                   i, h[kOhKind], h[kOhK], h[kOhNth], h[kOhNsec], h[kOhT], h[kOhNgrp], h[kOhMaxr], h[kOhDot],
+                   h[kOhNo1], h[kOhNf], h[kOhNs]);
+    }
+  }
   out.plan = I;
   return out;
 }
 
 // ints of the fast region after its complex and double buffers: dims, block
 // offsets, kept counts, kept eigenvector index table, flags; then the plan image
-constexpr int kFastDbl = 64 + 64 + 8;  // LAM, SIG, spare
+constexpr int kFastDbl = 64 + 64 + 64 + 8;  // LAM, SIG, 1 / SIG, spare
 inline int fast_int_words(const OcgParams& P, int nblk) {
   auto al = [](int x) { return (x + 3) & ~3; };
   return al(P.nsq) + al(nblk) + 64 /* KQ */ + 64 /* WIDX */ + 4 /* flags */;

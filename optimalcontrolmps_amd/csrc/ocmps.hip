@@ -202,7 +202,7 @@ struct ocg_ctx {
   std::string err;
   // HBM engine getHessian path counters (ocg_kernel_stats kind 8): pipelined
   // calls completed, and two-phase retries after a pipeline that ran out of memory
-  long pipe_runs = 0, pipe_fallbacks = 0;
+  long pipe_runs = 0, pipe_fallbacks = 0, ckpt_runs = 0, ckpt_k = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evh[4] = {nullptr, nullptr, nullptr, nullptr};  // ocg_hessian phase marks
@@ -1313,7 +1313,12 @@ int ocg_hessian(ocg_ctx* c, const double* u, int N, const int* rows, int nrows, 
     if (K > 0) {
       c->u_psi.clear();
       c->u_xi.clear();
-      return hb(c, hbm_hessian_ckpt(c->hbm, u, N, rows, nrows, H, divT, F, K));
+      const int rc = hb(c, hbm_hessian_ckpt(c->hbm, u, N, rows, nrows, H, divT, F, K));
+      if (rc == 0) {
+        ++c->ckpt_runs;
+        c->ckpt_k = K;
+      }
+      return rc;
     }
     // pipelined (psi + rows || dH || xi on three streams) when the row states fit
     // half the free HBM and the trajectories of u are not already on the device
@@ -1629,8 +1634,8 @@ int ocg_kernel_stats(ocg_ctx* c, int kind, double* total_ms, long* launches, dou
   if (kind == 8) {  // getHessian path counters (HBM engine; zeros on the LDS engine)
     if (total_ms) *total_ms = 0;
     if (launches) *launches = c->pipe_runs;
-    if (alg_bytes) *alg_bytes = 0;
-    if (alg_flops) *alg_flops = 0;
+    if (alg_bytes) *alg_bytes = double(c->ckpt_k);
+    if (alg_flops) *alg_flops = double(c->ckpt_runs);
     if (sweep_steps) *sweep_steps = c->pipe_fallbacks;
     return 0;
   }
@@ -1674,7 +1679,7 @@ int ocg_profile(ocg_ctx* c, double* out32, int reset) {
 
 int ocg_reset_stats(ocg_ctx* c) {
   if (!c) return OCG_EINVAL;
-  c->pipe_runs = c->pipe_fallbacks = 0;
+  c->pipe_runs = c->pipe_fallbacks = c->ckpt_runs = c->ckpt_k = 0;
   if (c->hbm) {
     hbm_reset_stats(c->hbm);
     return 0;

@@ -114,6 +114,7 @@ inline void emu_atomic_store(T* p, U v) {
 #define __builtin_amdgcn_s_sleep(x) ((void)0)
 inline void __threadfence() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
 #define __builtin_amdgcn_readlane(v, l) emu_readlane((v), (l))
+#define __builtin_amdgcn_readfirstlane(v) (v)  // every use reads a wave-uniform value
 #define __builtin_amdgcn_rcpf(x) emu_rcpf(x)
 #define __builtin_amdgcn_update_dpp(o, s, c, r, b, bc) emu_update_dpp((o), (s), (c), (r), (b), (bc))
 #define __builtin_amdgcn_fence(o, s) __atomic_thread_fence(__ATOMIC_SEQ_CST)

@@ -163,6 +163,37 @@ def test_c5_w512_pipelined_equals_stored(warm512, monkeypatch):
     assert np.array_equal(H0, H1) and np.array_equal(d0, d1) and F0 == F1
 
 
+def test_c5_w512_checkpointed_equals_stored(warm512, monkeypatch):
+    """the trajectory-checkpointed getHessian (hbm_hessian_ckpt; what config 5's
+    N_t = 1001 selects on its own, as psi_t + xi_t + xiH_t exceed half of HBM)
+    at chi = 512, segment length 2, N_t = 6: bit for bit the stored two-phase
+    path, divT and F included; a row subset equals the matching rows"""
+    ini, tgt = warm512
+    nt = 6
+    u = np.random.default_rng(53).uniform(2.0, 10.0, nt)
+    rows = np.arange(1, nt - 1, dtype=np.int32)
+    out = {}
+    for k in ("0", "2"):
+        monkeypatch.setenv("OCG_HBM_PIPE", "0")
+        if k == "0":
+            monkeypatch.delenv("OCG_HBM_CKPT", raising=False)
+        else:
+            monkeypatch.setenv("OCG_HBM_CKPT", k)
+        eng = _engine()
+        eng.set_states(tgt, ini)
+        out[k] = eng.hessian(u, rows)
+        assert eng.stats(8)["alg_flops"] == (1 if k == "2" else 0)
+        if k == "2":
+            sub = rows[[0, 2]]
+            Hs, _, _ = eng.hessian(u, sub)
+        eng.close()
+    (H0, d0, F0), (H2, d2, F2) = out["0"], out["2"]
+    assert np.array_equal(H0, H2) and np.array_equal(d0, d2) and F0 == F2
+    for r in sub:
+        assert np.array_equal(Hs[r, r:nt - 2], H0[r, r:nt - 2])
+        assert np.array_equal(Hs[r:nt - 2, r], H0[r:nt - 2, r])
+
+
 def test_c5_w512_certified_vs_eigen_gauge(warm512, monkeypatch):
     ini, _ = warm512
     res = {}

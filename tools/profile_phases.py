@@ -44,7 +44,12 @@ for what in ["trajectory(2 chains x 200 steps)", "div_t+xi_dH", "hessian_rows(19
         if pr[i] > 0:
             print(f"   {n:12s} {pr[i]:.3e} ({100*pr[i]/tot:5.1f}%)")
     print(f"   (inside gauge moves: {pr[31]:.3e} = {100*pr[31]/max(tot,1):.1f}% of the cycles)")
-    if pr[21] > 0:
+    if pr[22] > 0:   # the one-wave padded chain's counters
+        nst = 400 if what.startswith("traj") else 1
+        print(f"   fast chain: decompositions {pr[22]:.0f} ({pr[22]/nst:.2f} per chain-step), jacobi calls "
+              f"{pr[21]:.0f}, sweeps/call {pr[20]/max(pr[21],1):.2f}, rounds/call {pr[30]/max(pr[21],1):.2f}, "
+              f"small eigenvalues per decomposition {pr[17]/pr[22]:.1f}")
+    elif pr[21] > 0:
         print(f"   jacobi calls {pr[21]:.0f}, sweeps/call {pr[20]/pr[21]:.2f}, rounds/sweep {pr[22]/pr[21]:.2f}, "
               f"rounds executed/call (wave 0 of the first block group) {pr[30]/pr[21]:.2f}")
 print("traj kernel ms:", eng.stats(0)["ms"], " rows ms:", eng.stats(3)["ms"])
