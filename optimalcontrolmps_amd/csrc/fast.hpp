@@ -53,7 +53,7 @@ enum {
   kOhNgrp, kOhMaxr,  // Jacobi groups, rounds per sweep (0, 1 or 3)
   kOhO1, kOhNo1,     // order-1 sectors: int4 {M offset, length, stride, eigen slot}
   kOhEq,             // eigen slot e: int4 {s, i, eoff of s, n of s | bound << 8}
-  kOhSecQ,           // sector s -> q of the rewritten bond (ints)
+  kOhSecQ,           // sector s: q | eigen offset << 8 | order << 16 (ints)
   kOhF, kOhNf,       // factor elements: int4 (see fast_plan.hpp)
   kOhS, kOhNs,       // gauge product elements: int4 {x1 | x2 << 16, len | s2 << 16, dest, 0}
   kOhDot,            // longest Gram / order-1 dot product of the decomposition

@@ -367,15 +367,35 @@ struct FastChain {
   __device__ OCG_INLINE void decompose(const LDS int* oh, lzp M, int dir, double cutoff, int maxm, bool normalize) {
     using namespace fastp;
     pf(2);
-    const int nsec = uni(oh[kOhNsec]), T = uni(oh[kOhT]), maxr = uni(oh[kOhMaxr]), no1 = uni(oh[kOhNo1]);
-    // ---- Gram of the Jacobi groups: lane 16 g + 4 i + j holds G[i][j]
+    // the op header in one batch of loads (every field wave-uniform), then every
+    // per-lane table entry the decomposition reads, before any arithmetic: the
+    // group descriptors, order-1 sectors, eigen slots, the rewritten bond's
+    // sectors and their current dims, the factor descriptors
+    const i4 h2 = ld4(oh + 8), h3 = ld4(oh + 12), h4 = ld4(oh + 16), h5 = ld4(oh + 20);
+    const int newb = uni(oh[kOhNewBond]);
+    const int nsec = uni(h2[kOhNsec - 8]), T = uni(h2[kOhT - 8]), maxr = uni(h3[kOhMaxr - 12]),
+              no1 = uni(h3[kOhNo1 - 12]), o_o1 = uni(h3[kOhO1 - 12]), o_eq = uni(h4[kOhEq - 16]),
+              o_secq = uni(h4[kOhSecQ - 16]), o_f = uni(h4[kOhF - 16]), nf = uni(h4[kOhNf - 16]),
+              dot = uni(h5[kOhDot - 20]);
     const int g = lane >> 4, i = (lane >> 2) & 3, j = lane & 3, rb = lane & ~15;
     const i4 ga = ld4(oh + kOhGrp + 8 * g), gb = ld4(oh + kOhGrp + 8 * g + 4);
+    const i4 o1 = ld4(PL + o_o1 + 4 * (lane < no1 ? lane : 0));
+    const bool ae = lane < T;
+    const i4 eq = ld4(PL + o_eq + 4 * (ae ? lane : 0));
+    const int sqe = PL[o_secq + (lane < nsec ? lane : 0)];  // q | eigen offset << 8 | n << 16
+    i4 fd[kItF];
+#pragma unroll
+    for (int it = 0; it < kItF; ++it) {
+      const int e = lane + 64 * it;
+      fd[it] = ld4(PL + o_f + 4 * (e < nf ? e : nf - 1));
+    }
+    const int at_q = newb * P.Q1 + (sqe & 255);
+    const int dold = DIM[at_q];
+    // ---- Gram of the Jacobi groups: lane 16 g + 4 i + j holds G[i][j]
     const bool used = ga[0] >= 0;
     const int n = used ? ga[1] : 0, side = ga[2], tho = ga[3], R = gb[0], C = gb[1], eoff = gb[2];
     const bool valid = i < n && j < n;
     // order-1 sectors (lanes < no1): the block's one row / column squared norm
-    const i4 o1 = ld4(PL + uni(oh[kOhO1]) + 4 * (lane < no1 ? lane : 0));
     // G[i][j] = sum_c a_c conj(b_c) on either side (cols side: the conjugate of
     // that sum); the loop is unrolled to the op's longest dot product (header,
     // uniform), indices beyond a block's length read the zero slot
@@ -386,7 +406,6 @@ struct FastChain {
       const int bi = side == 0 ? tho + (i < n ? i : 0) * C : tho + (i < n ? i : 0);
       const int bj = side == 0 ? tho + (j < n ? j : 0) * C : tho + (j < n ? j : 0);
       const int len1 = lane < no1 ? o1[1] : 0, b1 = o1[0], s1 = o1[2];
-      const int dot = uni(oh[kOhDot]);
       if (dot <= 4) gram_dots<4>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
       else if (dot <= 8) gram_dots<8>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
       else gram_dots<kMaxDot>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
@@ -407,10 +426,8 @@ struct FastChain {
     if (lane < no1) LAM[o1[3]] = lam1;
     wsync();
     // ---- truncation (Chain::decompose, one-wave form): eigen slot e = lane
-    const bool ae = lane < T;
-    const i4 eq = ld4(PL + uni(oh[kOhEq]) + 4 * (ae ? lane : 0));
     const double lam = ae ? LAM[lane] : 0.0;
-    const int s_e = eq[0], i_e = eq[1], eo_e = eq[2], n_e = eq[3] & 255, bound = unsigned(eq[3]) >> 8;
+    const int i_e = eq[1], eo_e = eq[2], n_e = eq[3] & 255, bound = unsigned(eq[3]) >> 8;
     // rank inside the block (descending, ties by index)
     // (all partner values fetched first; non-short-circuit predicates keep the
     // compares free of branches, so the four exchanges are in flight together)
@@ -474,20 +491,17 @@ struct FastChain {
       SIGI[eo_e + jb] = sq > 0 ? 1.0 / sq : 0.0;  // the factors' 1 / sigma, once per eigenvalue
     }
     const double kw = wsum(kept ? lam : 0.0);
-    int kq = 0;
-    for (int s = 0; s < nsec; ++s) {
-      const int c = __popcll(__ballot(kept && s_e == s));
-      kq = (lane == s) ? c : kq;
-    }
     {
-      const int newb = uni(oh[kOhNewBond]);
-      const int q = lane < nsec ? PL[uni(oh[kOhSecQ]) + lane] : 0;
+      // kept count of sector s = lane: the kept bits of its eigen slots
+      // [eoff, eoff + n) (consecutive, in sector order)
+      const unsigned long long K = __ballot(kept);
+      const int eo = (sqe >> 8) & 255, ns = (sqe >> 16) & 15;
+      const int kq = __popcll((K >> eo) & ((1ull << ns) - 1));
       bool changed = false;
       if (lane < nsec) {
-        const int at = newb * P.Q1 + q;
-        changed = DIM[at] != kq;
+        changed = dold != kq;
         KQ[lane] = kq;
-        DIM[at] = kq;
+        DIM[at_q] = kq;
       }
       if (__ballot(changed)) ++dims_epoch;
     }
@@ -495,14 +509,6 @@ struct FastChain {
     pf(5);
     // ---- factors (Chain::decompose's materialisation): X rows, Y cols
     const double inv = (normalize && kw > 1e-32) ? 1.0 / sqrt(kw) : 1.0;
-    const int nf = uni(oh[kOhNf]);
-    const LDS int* fl = PL + uni(oh[kOhF]);
-    i4 fd[kItF];
-#pragma unroll
-    for (int it = 0; it < kItF; ++it) {
-      const int e = lane + 64 * it;
-      fd[it] = ld4(fl + 4 * (e < nf ? e : nf - 1));
-    }
     // operands in two dependent waves of loads, all elements at once: (KQ, WIDX,
     // SIG, the M terms), then the eigenvector entries W[., wv]; branch-free
     // (an exact factor is a selected entry of W, a derived one sum_x M W)

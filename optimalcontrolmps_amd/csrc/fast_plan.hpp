@@ -282,7 +282,7 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
       for (int i = 0; i < secn[q]; ++i) push4(s, i, seceoff[q], secn[q] | (D(newb, q) << 8));
     }
     setH(kOhSecQ, pad());
-    for (int s = 0; s < nsec; ++s) I.push_back(sq[s]);
+    for (int s = 0; s < nsec; ++s) I.push_back(sq[s] | (seceoff[sq[s]] << 8) | (secn[sq[s]] << 16));
     // -- factor elements, int4:
     //   w0 = dest | s << 16 | j << 20 | isx << 24 | scratch << 25
     //   w1 = exact: W offset of row idx (grp 16 + 4 idx); derived: M offset of the
