@@ -596,7 +596,15 @@ struct FastChain {
   __device__ OCG_INLINE void jacobi(zc& g, zc& w, bool valid, int i, int j, int rb, int n, int maxr) {
     auto at = [&](int r, int c) { return (rb + r * 4 + c) << 2; };
     double di = CH::bperm(g.x, at(i, i)), dj = CH::bperm(g.x, at(j, j));
-    int arow[3], acol[3], fl[3];
+    // Lane (x, y) publishes the rotation coefficients of index x in the pair
+    // (x, y): J[x][x] and J[y][x].  A reader takes its column's from lane
+    // (j, pj) and its row's from lane (i, pi) -- the pivot (p, q) for p, its
+    // mirror (q, p) for q, a diagonal lane (identity) for an unpaired index.  The
+    // mirror evaluates the pivot's rotation from the pivot's own element (the
+    // DPP partner g11 = g[p][q] of this round) and the same diagonal pair, so
+    // both roles use one rotation, bit for bit; no reader selects a role.
+    int arow[3], acol[3];
+    bool zp[3];
 #pragma unroll
     for (int rnd = 0; rnd < 3; ++rnd) {
       const int k = rnd + 1;
@@ -605,11 +613,11 @@ struct FastChain {
         if ((i ^ k) < n) pi = i ^ k;
         if ((j ^ k) < n) pj = j ^ k;
       }
-      arow[rnd] = at(i < pi ? i : pi, i < pi ? pi : i);
-      acol[rnd] = at(j < pj ? j : pj, j < pj ? pj : j);
-      fl[rnd] = (i < j && pi == j ? 1 : 0) | (j < pj ? 2 : 0) | (i < pi ? 4 : 0) | (pj != j ? 8 : 0) |
-                (pi != i ? 16 : 0) | (pi == j ? 32 : 0);
+      arow[rnd] = at(i, pi);
+      acol[rnd] = at(j, pj);
+      zp[rnd] = pi == j && i != j;  // the lane holds its own pair's off-diagonal
     }
+    const bool up = i < j, dg = i == j;
     int sweep = 0, nr = 0;
     bool done = false;
     for (; sweep < 40; ++sweep) {
@@ -617,48 +625,43 @@ struct FastChain {
 #pragma unroll
       for (int rnd = 0; rnd < 3; ++rnd) {
         if (rnd >= maxr) break;
-        const int f = fl[rnd];
-        const bool need = CH::jneed(cabs2(g), di, dj);
-        if (__ballot(valid && i < j && need) == 0) {
+        if (__ballot(valid && up && CH::jneed(cabs2(g), di, dj)) == 0) {
           done = true;
           break;
         }
         ++nr;
-        zc cs, e;
-        double sh;
-        CH::jrot_fast(g, di, dj, need, cs, e, sh);
-        const bool piv = f & 1;
-        cs = piv ? cs : c2(1.0, 0.0);
-        sh = piv ? sh : 0.0;
-        const zc csj = CH::bpermz(cs, acol[rnd]), ej = CH::bpermz(e, acol[rnd]);
-        const zc csi = CH::bpermz(cs, arow[rnd]), ei = CH::bpermz(e, arow[rnd]);
-        const double shj = CH::bperm(sh, acol[rnd]), shi = CH::bperm(sh, arow[rnd]);
         const zc g01 = CH::xcol(g, rnd), g10 = CH::xrow(g, rnd);
         const zc g11 = CH::xrow(g01, rnd), w1 = CH::xcol(w, rnd);
-        const bool rotj = (f & 8) && csj.y != 0.0, roti = (f & 16) && csi.y != 0.0;
-        zc jjj, jpj, jii, jpi;
-        CH::jcol(f & 2, csj, ej, jjj, jpj);
-        CH::jcol(f & 4, csi, ei, jii, jpi);
-        jjj = rotj ? jjj : c2(1, 0);
-        jpj = rotj ? jpj : c2(0, 0);
-        jii = roti ? jii : c2(1, 0);
-        jpi = roti ? jpi : c2(0, 0);
-        zc wn = cmul(w, jjj);
-        cacc(wn, w1, jpj);
-        zc r0 = cmul(g, jjj);
-        cacc(r0, g01, jpj);
-        zc r1 = cmul(g10, jjj);
-        cacc(r1, g11, jpj);
-        zc out = cjmul(jii, r0);
-        cjacc(out, jpi, r1);
-        const bool zero = rotj && roti && (f & 32);
-        const bool diag = rotj && i == j;
-        out = zero ? c2(0, 0) : out;
-        out = diag ? c2(g.x + ((f & 2) ? -shj : shj), 0) : out;
+        const zc bv = up ? g : g11;  // the pivot element g[p][q] (for the mirror: its DPP partner)
+        const double app = up ? di : dj, aqq = up ? dj : di;
+        const bool need = CH::jneed(cabs2(bv), app, aqq);
+        zc cs, e;
+        double sh;
+        CH::jrot_fast(bv, app, aqq, need, cs, e, sh);
+        const zc ec = cconj(e);
+        zc jd = up ? c2(cs.x, 0.0) : cscale(ec, cs.x);   // p: c,        q: c e*
+        zc jo = up ? cscale(ec, -cs.y) : c2(cs.y, 0.0);  // p: -s e*,    q: s
+        double ds = up ? -sh : sh;                        // p: -shift,   q: +shift
+        jd = dg ? c2(1.0, 0.0) : jd;
+        jo = dg ? c2(0.0, 0.0) : jo;
+        ds = dg ? 0.0 : ds;
+        const zc jdc = CH::bpermz(jd, acol[rnd]), joc = CH::bpermz(jo, acol[rnd]);
+        const zc jdr = CH::bpermz(jd, arow[rnd]), jor = CH::bpermz(jo, arow[rnd]);
+        const double dsc = CH::bperm(ds, acol[rnd]), dsr = CH::bperm(ds, arow[rnd]);
+        // W' = W J, G' = J^H G J on the 2 x 2 super-block of (i, pi) x (j, pj)
+        zc wn = cmul(w, jdc);
+        cacc(wn, w1, joc);
+        zc r0 = cmul(g, jdc);
+        cacc(r0, g01, joc);
+        zc r1 = cmul(g10, jdc);
+        cacc(r1, g11, joc);
+        zc out = cjmul(jdr, r0);
+        cjacc(out, jor, r1);
         // the diagonal entries of this lane's row and column after the rotation
-        const double dj2 = rotj ? dj + ((f & 2) ? -shj : shj) : dj;
-        const double di2 = roti ? di + ((f & 4) ? -shi : shi) : di;
-        if (rnd == maxr - 1) flag = valid && i < j && CH::jneed(cabs2(out), di2, dj2);
+        const double dj2 = dj + dsc, di2 = di + dsr;
+        out = (zp[rnd] && need) ? c2(0.0, 0.0) : out;  // the rotated pair: exact zero
+        out = dg ? c2(dj2, 0.0) : out;                  // a diagonal entry: the shifted value
+        if (rnd == maxr - 1) flag = valid && up && CH::jneed(cabs2(out), di2, dj2);
         g = out;
         w = wn;
         di = di2;
