@@ -260,16 +260,24 @@ struct FastChain {
     using namespace fastp;
     pf(0);
     const int nth = uni(oh[kOhNth]);
+    if (nth <= 64) theta_it<1>(oh, nth);
+    else theta_it<kItTh>(oh, nth);
+    wsync();
+  }
+  // IT: 64-element iterations, unrolled (the op's element count picks the instance)
+  template <int IT>
+  __device__ OCG_INLINE void theta_it(const LDS int* oh, int nth) {
+    using namespace fastp;
     const LDS int* md = PL + uni(oh[kOhMat]);
-    int d0[kItTh], d1[kItTh];
+    int d0[IT], d1[IT];
 #pragma unroll
-    for (int it = 0; it < kItTh; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it, ee = e < nth ? e : nth - 1;
       d0[it] = md[2 * ee];
       d1[it] = md[2 * ee + 1];
     }
 #pragma unroll
-    for (int it = 0; it < kItTh; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it;
       const int x1 = d0[it] & 0xffff, x2 = unsigned(d0[it]) >> 16, dm = d1[it] & 0xff, drc = unsigned(d1[it]) >> 8;
       const int dmc = dm > 0 ? dm - 1 : 0;
@@ -282,7 +290,6 @@ struct FastChain {
       }
       if (e < nth) TH[e] = acc;
     }
-    wsync();
   }
   // pre-phase -> hopping gate (per Δ = n1 + n2 block) -> post-phase (Chain::apply_gate).
   // PH holds UF[p], UT[p], then the pair products UF[n1] UF[n2] and UT[a1] UT[a2] (p^2 each)
@@ -292,30 +299,35 @@ struct FastChain {
     using namespace fastp;
     pf(1);
     const int mode = uni(oh[kOhMode]), lonely = uni(oh[kOhLonely]);
-    if (mode == 0) {
-      if (lonely & 1) gate_body<1, 2>(oh, forward);
-      else gate_body<1, 0>(oh, forward);
-    } else {
-      if (lonely & 2) gate_body<2, 1>(oh, forward);
-      else gate_body<0, 1>(oh, forward);
-    }
+    if (uni(oh[kOhNth]) <= 64) gate_mode<1>(oh, forward, mode, lonely);
+    else gate_mode<kItTh>(oh, forward, mode, lonely);
     wsync();
   }
-  template <int PRE, int POST>
+  template <int IT>
+  __device__ OCG_INLINE void gate_mode(const LDS int* oh, int forward, int mode, int lonely) {
+    if (mode == 0) {
+      if (lonely & 1) gate_body<1, 2, IT>(oh, forward);
+      else gate_body<1, 0, IT>(oh, forward);
+    } else {
+      if (lonely & 2) gate_body<2, 1, IT>(oh, forward);
+      else gate_body<0, 1, IT>(oh, forward);
+    }
+  }
+  template <int PRE, int POST, int IT>
   __device__ OCG_INLINE void gate_body(const LDS int* oh, int forward) {
     using namespace fastp;
     const int p = P.p, nth = uni(oh[kOhNth]);
     const LDS int* gd = PL + uni(oh[kOhGate]);
     lzp g0 = GT + (forward ? 0 : P.gtotal);
     lzp UF = PH, UT = PH + p, UFF = PH + 2 * p, UTT = PH + 2 * p + p * p;
-    i4 d[kItTh];
+    i4 d[IT];
 #pragma unroll
-    for (int it = 0; it < kItTh; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it;
       d[it] = ld4(gd + 4 * (e < nth ? e : nth - 1));
     }
 #pragma unroll
-    for (int it = 0; it < kItTh; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it;
       const unsigned h = d[it][0];
       const int sz = (h >> 16) & 15, lo = (h >> 20) & 15, a1 = (h >> 24) & 15, a2 = h >> 28, D = a1 + a2;
@@ -342,20 +354,26 @@ struct FastChain {
     using namespace fastp;
     pf(7);
     const int nth = uni(oh[kOhNth]);
+    if (nth <= 64) matcopy_it<1>(oh, nth);
+    else matcopy_it<kItTh>(oh, nth);
+    wsync();
+  }
+  template <int IT>
+  __device__ OCG_INLINE void matcopy_it(const LDS int* oh, int nth) {
+    using namespace fastp;
     const LDS int* src = PL + uni(oh[kOhMat]);
-    int s[kItTh];
+    int s[IT];
 #pragma unroll
-    for (int it = 0; it < kItTh; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it;
       s[it] = src[e < nth ? e : nth - 1];
     }
 #pragma unroll
-    for (int it = 0; it < kItTh; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it;
       const zc v = MP[s[it]];
       if (e < nth) TH[e] = v;
     }
-    wsync();
   }
 
   // ------------------------------------------------------------- decomposition
@@ -383,12 +401,6 @@ struct FastChain {
     const bool ae = lane < T;
     const i4 eq = ld4(PL + o_eq + 4 * (ae ? lane : 0));
     const int sqe = PL[o_secq + (lane < nsec ? lane : 0)];  // q | eigen offset << 8 | n << 16
-    i4 fd[kItF];
-#pragma unroll
-    for (int it = 0; it < kItF; ++it) {
-      const int e = lane + 64 * it;
-      fd[it] = ld4(PL + o_f + 4 * (e < nf ? e : nf - 1));
-    }
     const int at_q = newb * P.Q1 + (sqe & 255);
     const int dold = DIM[at_q];
     // ---- Gram of the Jacobi groups: lane 16 g + 4 i + j holds G[i][j]
@@ -509,14 +521,30 @@ struct FastChain {
     pf(5);
     // ---- factors (Chain::decompose's materialisation): X rows, Y cols
     const double inv = (normalize && kw > 1e-32) ? 1.0 / sqrt(kw) : 1.0;
+    if (nf <= 64) factors<1>(o_f, nf, M, dir, inv);
+    else if (nf <= 128) factors<2>(o_f, nf, M, dir, inv);
+    else if (nf <= 192) factors<3>(o_f, nf, M, dir, inv);
+    else factors<kItF>(o_f, nf, M, dir, inv);
+  }
+
+  // factor elements (IF 64-element iterations; the op's count picks the instance)
+  template <int IF>
+  __device__ OCG_INLINE void factors(int o_f, int nf, lzp M, int dir, double inv) {
+    using namespace fastp;
+    i4 fd[IF];
+#pragma unroll
+    for (int it = 0; it < IF; ++it) {
+      const int e = lane + 64 * it;
+      fd[it] = ld4(PL + o_f + 4 * (e < nf ? e : nf - 1));
+    }
     // operands in two dependent waves of loads, all elements at once: (KQ, WIDX,
     // SIG, the M terms), then the eigenvector entries W[., wv]; branch-free
     // (an exact factor is a selected entry of W, a derived one sum_x M W)
-    int kqs[kItF], wvv[kItF];
-    double sg[kItF], isg[kItF];
-    zc mv[kItF][kMaxGram];
+    int kqs[IF], wvv[IF];
+    double sg[IF], isg[IF];
+    zc mv[IF][kMaxGram];
 #pragma unroll
-    for (int it = 0; it < kItF; ++it) {
+    for (int it = 0; it < IF; ++it) {
       const int w0 = fd[it][0], w1 = fd[it][1], w2 = fd[it][2];
       const int s = (w0 >> 16) & 15, jj = (w0 >> 20) & 15, eo = w2 & 255;
       const bool exact = (w2 >> 12) & 1;
@@ -528,10 +556,10 @@ struct FastChain {
 #pragma unroll
       for (int x = 0; x < kMaxGram; ++x) mv[it][x] = M[(exact || x >= terms) ? thz : mb + x * ms];
     }
-    zc out[kItF];
-    int dst[kItF];
+    zc out[IF];
+    int dst[IF];
 #pragma unroll
-    for (int it = 0; it < kItF; ++it) {
+    for (int it = 0; it < IF; ++it) {
       const int e = lane + 64 * it;
       const int w0 = fd[it][0], w1 = fd[it][1], w2 = fd[it][2], wbse = fd[it][3];
       const int dest = w0 & 0xffff, jj = (w0 >> 20) & 15;
@@ -565,7 +593,7 @@ struct FastChain {
     }
     pf(23);
 #pragma unroll
-    for (int it = 0; it < kItF; ++it)
+    for (int it = 0; it < IF; ++it)
       if (dst[it] >= 0) ((dst[it] >> 16) ? XS : MP)[dst[it] & 0xffff] = out[it];
     wsync();
   }
@@ -684,16 +712,23 @@ struct FastChain {
     using namespace fastp;
     pf(25);
     const int ns = uni(oh[kOhNs]), kind = uni(oh[kOhKind]);
+    if (ns <= 64) neighbour_it<1>(oh, ns, kind);
+    else if (ns <= 128) neighbour_it<2>(oh, ns, kind);
+    else neighbour_it<kItS>(oh, ns, kind);
+  }
+  template <int IT>
+  __device__ OCG_INLINE void neighbour_it(const LDS int* oh, int ns, int kind) {
+    using namespace fastp;
     const LDS int* sl = PL + uni(oh[kOhS]);
-    i4 d[kItS];
+    i4 d[IT];
 #pragma unroll
-    for (int it = 0; it < kItS; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int e = lane + 64 * it;
       d[it] = ld4(sl + 4 * (e < ns ? e : ns - 1));
     }
-    zc acc[kItS];
+    zc acc[IT];
 #pragma unroll
-    for (int it = 0; it < kItS; ++it) {
+    for (int it = 0; it < IT; ++it) {
       const int x1 = d[it][0] & 0xffff, x2 = unsigned(d[it][0]) >> 16, len = d[it][1] & 0xffff,
                 s2 = unsigned(d[it][1]) >> 16;
       const int lc = len > 0 ? len - 1 : 0;
@@ -709,7 +744,7 @@ struct FastChain {
     }
     wsync();
 #pragma unroll
-    for (int it = 0; it < kItS; ++it)
+    for (int it = 0; it < IT; ++it)
       if (lane + 64 * it < ns) MP[d[it][2]] = acc[it];
     wsync();
   }

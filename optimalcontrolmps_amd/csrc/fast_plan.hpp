@@ -411,6 +411,7 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
   I[kHNint] = int(I.size());
   if (I.size() > 65535) return fail("plan too large");
   if (std::getenv("OCG_FAST_DUMP")) {  // diagnostic: the step's operations
+    std::fprintf(stderr, "[fast plan] np %d nblk %d ints %zu zc %d\n", np, nblk, I.size(), zc_off);
     for (size_t i = 0; i < ops.size(); ++i) {
       const int* h = &I[op_off[i]];
       std::fprintf(stderr, "[fast plan] op %zu kind %d k %d nth %d nsec %d T %d ngrp %d maxr %d dot %d no1 %d nf %d ns %d\n",

@@ -2757,7 +2757,9 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
     std::vector<int> rs(rows, rows + nrows);
     std::sort(rs.begin(), rs.end());
     const int B = std::max(1, hbm_batch(h, std::max(nrows, 1)));
-    E.reserve_chains(std::max(E.nchain_cap, std::max(B, 2)), false);
+    // in flight at once: the batch's row chains, a segment's xiH outputs (<= K)
+    // and the two recomputation chains
+    E.reserve_chains(std::max(E.nchain_cap, B + K + 2), false);
     bool first = true;
     for (int r0 = 0; first || r0 < nrows; r0 += B) {
       const int nb = std::min(B, nrows - r0);
@@ -2771,29 +2773,23 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
         const int a = Tc(s), b = Tc(s + 1);  // segment [a, b]
         const bool need_rows = nb > 0 && b - 1 >= imin && a <= N - 2;
         if (!first && !need_rows) continue;
-        // psi_a..psi_b forward from the checkpoint
+        // psi_a..psi_b forward and xi_b..xi_a backward from their checkpoints, one
+        // batch of two chains (every HBM-engine kernel is batch-independent: the
+        // same states as two single-chain passes, in half the dependent steps)
         {
-          std::vector<Chain*> c1{E.acquire(false)};
-          E.load_many(c1, {E.states[ckp + s].view()});
-          E.store_many({&E.states[sgp]}, c1);
-          for (int t = a; t < b; ++t) {
-            E.step(c1, {u[t]}, {u[t + 1]}, {1});
-            E.store_many({&E.states[sgp + t + 1 - a]}, c1);
+          std::vector<Chain*> c2{E.acquire(false), E.acquire(false)};
+          E.load_many(c2, {E.states[ckp + s].view(), E.states[ckx + s + 1].view()});
+          E.store_many({&E.states[sgp], &E.states[sgx + b - a]}, c2);
+          std::vector<double> uf(2), ut(2);
+          const std::vector<int> fw{1, 0};
+          for (int m = 0; m < b - a; ++m) {
+            uf[0] = u[a + m]; ut[0] = u[a + m + 1];
+            uf[1] = u[b - m]; ut[1] = u[b - m - 1];
+            E.step(c2, uf, ut, fw);
+            E.store_many({&E.states[sgp + m + 1], &E.states[sgx + b - m - 1 - a]}, c2);
           }
           E.sync();
-          E.release(c1[0]);
-        }
-        // xi_b..xi_a backward from the checkpoint
-        {
-          std::vector<Chain*> c1{E.acquire(false)};
-          E.load_many(c1, {E.states[ckx + s + 1].view()});
-          E.store_many({&E.states[sgx + b - a]}, c1);
-          for (int t = b; t > a; --t) {
-            E.step(c1, {u[t]}, {u[t - 1]}, {0});
-            E.store_many({&E.states[sgx + t - 1 - a]}, c1);
-          }
-          E.sync();
-          E.release(c1[0]);
+          for (auto* c : c2) E.release(c);
         }
         // divT_t = overlapC(xi_t, dH, psi_t) (:409-419), t in [a, b) (and N-1 at the end)
         if (first) {
