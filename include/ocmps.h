@@ -169,6 +169,17 @@ int ocg_hessian(ocg_ctx* ctx, const double* u, int N, const int* rows, int nrows
  * F: K x 2.  Leaves control 0's trajectories as ocg_hessian would. */
 int ocg_hessian_multi(ocg_ctx* ctx, int K, const double* u, int N, const int* rows, int nrows, double* H,
                       double* divT, double* F);
+/* getAnalyticGradient's device work for one control vector (calcPsi || calcXi,
+ * calcDivT and F = <psi_{N-1}|psi_target>, src/OptimalControl.cpp:204-249,
+ * :375-419): divT (2N doubles, complex) and F (2 doubles).  = ocg_propagate(..,3)
+ * + ocg_div_t + ocg_overlap_factor, whose trajectories it leaves on the device,
+ * unless the HBM engine's stored trajectories would not fit half the free HBM
+ * (config 5 at N_t = 1001): then psi and xi run as one lockstep batch that
+ * meets in the middle (psi_0..psi_{N/2} and xi_{N/2+1}..xi_{N-1} stored, the
+ * other halves paired as they are produced): N states instead of 2N, the same
+ * N-1 dependent steps, the same numbers bit for bit, no trajectories left
+ * (OCG_HBM_MID=1 / 0 forces either path). */
+int ocg_gradient(ocg_ctx* ctx, const double* u, int N, double* divT, double* F);
 /* The gradient's device work (calcPsi || calcXi + divT + F, the BFGS path of
  * calcFidelityGrad, src/OptimalControl.cpp:204-249) for K control vectors
  * u[k*N .. k*N+N) in one call: LDS engine, one trajectory launch of 2K chains

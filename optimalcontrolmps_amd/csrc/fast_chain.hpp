@@ -40,7 +40,8 @@ struct FastChain {
   const int lane;
   const bool act;  // wave 0
   lzp MP, TH, TG, WB, XS, GT, PH;
-  LDS double *LAM, *SIG, *SIGI;
+  LDS double *LAM, *SIG, *SIGI, *MCB, *MCF;
+  LDS int* MCE;
   LDS int *DIM, *BOF, *KQ, *WIDX, *PL;
   int np, nblk, o_blk, o_ls, o_site, o_siten, nops, centre_open;
   int thz, xsz;  // zero slots of TH / TG and XS (MP's is np)
@@ -94,7 +95,9 @@ struct FastChain {
     XS = cb + gplan[kHZX]; GT = cb + gplan[kHZGt]; PH = cb + gplan[kHZPh];
     LDS double* db = (cb + gplan[kHZTot]).p;
     LAM = db; SIG = db + 64; SIGI = db + 128;  // then 8 spare doubles
-    LDS int* ib = (LDS int*)(db + 200);
+    MCB = db + 200; MCF = db + 200 + fastp::kMaxOps;  // the traffic model's per-op cache
+    LDS int* ib = (LDS int*)(db + 200 + 2 * fastp::kMaxOps);
+    MCE = ib; ib += fastp::kMaxOps;
     auto al = [](int x) { return (x + 3) & ~3; };  // 16-byte aligned int arrays
     DIM = ib; ib += al(P.nsq);
     BOF = ib; ib += al(nblk);
@@ -117,6 +120,7 @@ struct FastChain {
     const int ni = gplan[fastp::kHNint];
     for (int i = lane; i < ni; i += 64) PL[i] = gplan[i];
     for (int i = lane; i < P.gtotal; i += 64) { GT[i] = gf[i]; GT[P.gtotal + i] = gb[i]; }
+    if (lane < fastp::kMaxOps) MCE[lane] = -1;
     if (lane == 0) {
       WB[64] = c2(1.0, 0.0);  // the eigenvector of every order-1 sector
       MP[np] = c2(0.0, 0.0);  // zero slots
@@ -218,7 +222,18 @@ struct FastChain {
   // the traffic model of one two-site update on the current (unpadded) dims:
   // 16 (2 (|A_i1| + |A_i2|) + gate) bytes, 8 (R C m + R C p + n^2 max(R, C) +
   // 2 R C m) flops per middle sector (Chain::build_theta's accounting)
-  __device__ OCG_INLINE void model_gate(int i1) {
+  // The model depends only on the bond dims at the gate, so an op's wave total
+  // is cached with the dims epoch it was formed at and reused while no bond
+  // dimension has changed since (every step once config 1's dims saturate).
+  __device__ OCG_INLINE void model_gate(int o, int i1) {
+    using namespace fastp;
+    if (uni(MCE[o]) == dims_epoch) {
+      if (lane == 0) {
+        m_bytes += MCB[o];
+        m_flops += MCF[o];
+      }
+      return;
+    }
     // all 3 p bond dims of the three bonds in one wave of loads (clamped
     // addresses, out-of-range sectors selected to 0)
     const int p = P.p, Q = P.Q, Q1 = P.Q1, q = lane < Q1 ? lane : 0;
@@ -251,8 +266,14 @@ struct FastChain {
       by = 32.0 * double(u);
     }
     if (lane == 0) by += 16.0 * P.gtotal;
-    m_bytes += by;
-    m_flops += fl;
+    const double bt = wsum(by), ft = wsum(fl);
+    if (lane == 0) {
+      m_bytes += bt;
+      m_flops += ft;
+      MCB[o] = bt;
+      MCF[o] = ft;
+      MCE[o] = dims_epoch;
+    }
   }
 
   // ------------------------------------------------------------- Θ and gate
@@ -425,9 +446,6 @@ struct FastChain {
     }
     if (!valid) gv = c2(0.0, 0.0);
     zc w = c2(i == j ? 1.0 : 0.0, 0.0);
-#ifdef OCG_FAST_TRACE
-    if (trace_op == 1 && valid) printf("[gram] grp %d side %d n %d R %d C %d (%d,%d) %.3e %.3e\n", g, side, n, R, C, i, j, gv.x, gv.y);
-#endif
     pf(3);
     if (maxr > 0) jacobi(gv, w, valid, i, j, rb, n, maxr);
     cnt(22, 1.0);
@@ -790,7 +808,7 @@ struct FastChain {
       trace_op = o;
       if (kind == kOpGate) {
         pf(12);
-        model_gate(uni(h0[1]));
+        model_gate(o, uni(h0[1]));
         theta(oh);
         gate(oh, forward);
         decompose(oh, TG, dir, P.cutoff, P.maxm, true);

@@ -425,10 +425,10 @@ inline FastPlanBuild build_fast_plan(const OcgParams& P, const std::vector<int>&
 
 // ints of the fast region after its complex and double buffers: dims, block
 // offsets, kept counts, kept eigenvector index table, flags; then the plan image
-constexpr int kFastDbl = 64 + 64 + 64 + 8;  // LAM, SIG, 1 / SIG, spare
+constexpr int kFastDbl = 64 + 64 + 64 + 8 + 2 * ocg::fastp::kMaxOps;  // LAM, SIG, 1 / SIG, spare, model cache
 inline int fast_int_words(const OcgParams& P, int nblk) {
   auto al = [](int x) { return (x + 3) & ~3; };
-  return al(P.nsq) + al(nblk) + 64 /* KQ */ + 64 /* WIDX */ + 4 /* flags */;
+  return ocg::fastp::kMaxOps /* model cache epochs */ + al(P.nsq) + al(nblk) + 64 /* KQ */ + 64 /* WIDX */ + 4 /* flags */;
 }
 inline int fast_lds_bytes(const std::vector<int>& plan, const OcgParams& P) {
   using namespace ocg::fastp;

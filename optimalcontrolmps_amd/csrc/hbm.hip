@@ -2488,6 +2488,83 @@ int hbm_div_t(hbm_engine* h, double* divT) {
   });
 }
 
+// getAnalyticGradient's device part (divT_t, F) without keeping the
+// trajectories: psi forward and xi backward run as one lockstep batch and meet
+// in the middle.  Phase 1 stores psi_0..psi_tm and xi_{N-1}..xi_{tm+1}
+// (tm = (N-1)/2); phase 2 carries psi on to N-1, each new psi_t paired with the
+// stored xi_t, and xi down to 0, each new xi_t paired with the stored psi_t.
+// N states instead of the stored path's 2N (config 5 at N_t = 1001: 205 GB
+// instead of 410 GB), the same N-1 dependent steps per chain, and the same
+// states, overlaps and numbers bit for bit (every HBM-engine kernel is
+// batch-independent and deterministic).  Leaves no device trajectories.
+int hbm_gradient_mid(hbm_engine* h, const double* u, int N, double* divT, double* F) {
+  return guard(h, [&] {
+    if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
+    if (N < 2) throw hbm::Error(1, "N < 2");
+    hbm::Engine& E = *h->E;
+    h->have_psi = h->have_xi = h->have_xih = false;  // the trajectory slots are overwritten
+    h->N = 0;
+    E.reserve_states(size_t(N) + 2);
+    const int tm = (N - 1) / 2;
+    auto slot = [](int t) { return 2 + t; };  // psi_t for t <= tm, xi_t above
+    E.reserve_chains(std::max(E.nchain_cap, 2), false);
+    Timer tt(h, 0);
+    Chain* cp = E.acquire(false);
+    Chain* cx = E.acquire(false);
+    std::vector<Chain*> both{cp, cx};
+    E.load_many(both, {E.states[0].view(), E.states[1].view()});
+    E.store_many({&E.states[slot(0)], &E.states[slot(N - 1)]}, both);
+    std::vector<std::complex<double>> dv(N);
+    long nsteps = 0;
+    // one lockstep step of the chains still moving: psi t -> t+1 while t < pe,
+    // xi t -> t-1 while t > xe
+    auto advance = [&](int& tp, int pe, int& tx, int xe) {
+      std::vector<Chain*> c;
+      std::vector<double> uf, ut;
+      std::vector<int> fw;
+      if (tp < pe) { c.push_back(cp); uf.push_back(u[tp]); ut.push_back(u[tp + 1]); fw.push_back(1); }
+      if (tx > xe) { c.push_back(cx); uf.push_back(u[tx]); ut.push_back(u[tx - 1]); fw.push_back(0); }
+      E.step(c, uf, ut, fw);
+      nsteps += long(c.size());
+      if (tp < pe) ++tp;
+      if (tx > xe) --tx;
+    };
+    // phase 1: psi 0 -> tm, xi N-1 -> tm+1, both stored
+    int tp = 0, tx = N - 1;
+    while (tp < tm || tx > tm + 1) {
+      const bool mp = tp < tm, mx = tx > tm + 1;
+      advance(tp, tm, tx, tm + 1);
+      std::vector<State*> ss;
+      std::vector<Chain*> cc;
+      if (mp) { ss.push_back(&E.states[slot(tp)]); cc.push_back(cp); }
+      if (mx) { ss.push_back(&E.states[slot(tx)]); cc.push_back(cx); }
+      E.store_many(ss, cc);
+    }
+    // phase 2: psi tm -> N-1 against the stored xi_t, xi tm+1 -> 0 against the stored psi_t
+    while (tp < N - 1 || tx > 0) {
+      const bool mp = tp < N - 1, mx = tx > 0;
+      advance(tp, N - 1, tx, 0);
+      std::vector<View> xs, ys;  // divT_t = overlapC(xi_t, dH, psi_t) (src/OptimalControl.cpp:409-419)
+      if (mp) { xs.push_back(E.states[slot(tp)].view()); ys.push_back(cp->view()); }
+      if (mx) { xs.push_back(cx->view()); ys.push_back(E.states[slot(tx)].view()); }
+      const auto r = E.overlaps(xs, ys, true);
+      int k = 0;
+      if (mp) dv[tp] = r[k++];
+      if (mx) dv[tx] = r[k++];
+    }
+    // F = overlapC(psi_{N-1}, target) (:242); the two end points of the trajectories
+    // (divT_{N-1} with xi_{N-1} = target, divT_0 with psi_0 = init) came from phase 2
+    const std::complex<double> Fc = E.overlaps({cp->view()}, {E.states[1].view()}, false)[0];
+    E.sync();
+    E.release(cp);
+    E.release(cx);
+    tt.stop(nsteps);
+    F[0] = Fc.real();
+    F[1] = Fc.imag();
+    for (int t = 0; t < N; ++t) { divT[2 * t] = dv[t].real(); divT[2 * t + 1] = dv[t].imag(); }
+  });
+}
+
 // K controls' psi || xi in one lockstep batch of 2K chains, then their divT and F
 // in two batched overlap launches (ocg_gradient_multi).  Control 0 uses the
 // context's trajectory slots, control k >= 1 the 2N slots after xiH's block.

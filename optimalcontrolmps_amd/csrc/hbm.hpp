@@ -42,6 +42,9 @@ int hbm_gradient_multi(hbm_engine* h, int K, const double* U, int N, double* div
 int hbm_xi_dH(hbm_engine* h);
 int hbm_hessian_rows(hbm_engine* h, const double* u, int N, const int* rows, int nrows, const double* F,
                      const double* divT, double* H);
+// divT_t and F without stored trajectories: psi || xi meeting in the middle,
+// N states instead of 2 N, bit-identical to propagate + div_t + overlap_factor
+int hbm_gradient_mid(hbm_engine* h, const double* u, int N, double* divT, double* F);
 // getHessian's fidelity part (psi, xi, divT, F, rows) with trajectory
 // checkpointing: psi_t / xi_t kept only every K steps,
 // segments recomputed, xiHlist formed one segment at a time; O(N/K + K + rows

@@ -1070,6 +1070,31 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
   return 0;
 }
 
+int ocg_gradient(ocg_ctx* c, const double* u, int N, double* divT, double* F) {
+  if (!c || !u || !divT || !F || N < 2) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
+  if (c->hbm) {
+    // the stored trajectories when psi_t + xi_t + xiH_t fit half the free HBM (they
+    // stay for eval_h's reuse), else psi || xi meeting in the middle (N states);
+    // OCG_HBM_MID=1 / 0 forces either
+    const char* e = std::getenv("OCG_HBM_MID");
+    int mid = e ? std::atoi(e) : -1;
+    if (mid < 0) {
+      size_t fr = 0, tot = 0;
+      HIPCHK(c, hipSetDevice(c->device));
+      HIPCHK(c, hipMemGetInfo(&fr, &tot));
+      mid = hbm_traj_bytes(c->hbm, N) > 0.5 * double(fr) ? 1 : 0;
+    }
+    if (mid == 1) {
+      c->u_psi.clear();
+      c->u_xi.clear();
+      return hb(c, hbm_gradient_mid(c->hbm, u, N, divT, F));
+    }
+  }
+  if (int rc = ocg_propagate(c, u, N, 3)) return rc;
+  if (int rc = ocg_div_t(c, divT)) return rc;
+  return ocg_overlap_factor(c, F);
+}
+
 int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, double* F) {
   if (!c || !u || !divT || !F || N < 2 || K < 1) return c ? fail(c, OCG_EINVAL, "bad argument") : OCG_EINVAL;
   if (size_t(K) * 4 * size_t(N) + 6 > size_t(INT32_MAX)) return fail(c, OCG_EINVAL, "K * N too large");

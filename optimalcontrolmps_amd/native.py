@@ -114,6 +114,7 @@ SIGNATURES = [
     ("ocg_hessian", C.c_int, [C.c_void_p, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_hessian_multi", C.c_int, [C.c_void_p, C.c_int, dp, C.c_int, ip, C.c_int, dp, dp, dp]),
     ("ocg_gradient_multi", C.c_int, [C.c_void_p, C.c_int, dp, C.c_int, dp, dp]),
+    ("ocg_gradient", C.c_int, [C.c_void_p, dp, C.c_int, dp, dp]),
     ("ocg_get_state", C.c_int, [C.c_void_p, C.c_int, C.c_int, ip, dp, C.c_size_t, szp]),
     ("ocg_convert_hessian", C.c_int, [C.c_void_p, dp, C.c_int, dp, C.c_int, dp]),
     ("ocg_denmat_decomp", C.c_int, [C.c_void_p, C.c_int, ip, ip, C.POINTER(dp), C.c_double, C.c_int, ip,
@@ -370,6 +371,18 @@ class Engine:
         self._chk(lib().ocg_hessian_multi(self.h, K, Um.ctypes.data_as(dp), N, pr, len(r), H.ctypes.data_as(dp),
                                           dv.ctypes.data_as(dp), Fa.ctypes.data_as(dp)), "ocg_hessian_multi")
         return H, dv.view(np.complex128).copy(), Fa[:, 0] + 1j * Fa[:, 1]
+
+    def gradient(self, u):
+        """getAnalyticGradient's device part for one control (ocg_gradient):
+        returns (divT (N,), F); on the HBM engine, when the stored trajectories
+        would not fit, psi || xi meet in the middle and none are kept"""
+        uu, pu = _d(u)
+        N = len(uu)
+        dv = np.zeros(2 * N)
+        Fa = np.zeros(2)
+        self._chk(lib().ocg_gradient(self.h, pu, N, dv.ctypes.data_as(dp), Fa.ctypes.data_as(dp)), "ocg_gradient")
+        self.N = N
+        return dv.view(np.complex128).copy(), complex(Fa[0], Fa[1])
 
     def gradient_multi(self, U):
         """psi || xi + divT + F for K control vectors (rows of U) in one call:

@@ -72,3 +72,50 @@ def test_ckpt_config4_s32_vs_oracle():
     assert np.array_equal(H1, H2) and np.array_equal(d1, d2) and F1 == F2
     Ho = c4["s32/H"]
     assert np.abs(H2 - Ho).max() <= 1e-6 * np.abs(Ho).max()
+
+
+def _mid(eng, u, mode):
+    os.environ["OCG_HBM_MID"] = mode
+    try:
+        return eng.gradient(u)
+    finally:
+        del os.environ["OCG_HBM_MID"]
+
+
+@pytest.mark.parametrize("N", [2, 3, 20, 21])
+def test_gradient_meet_in_the_middle_bitwise(states, N):
+    """ocg_gradient's memory-lean path (psi || xi meeting in the middle, N states
+    instead of 2N: config 5 at N_t = 1001) == propagate + div_t + overlap_factor
+    bit for bit, odd and even N, down to N = 2"""
+    from optimalcontrolmps_amd.native import MPS, Engine
+    L, p, Q, J = 5, 5, 5, 1.0
+
+    def st(U):
+        k = state_key(L, p, Q, J, U)
+        return MPS(L, p, Q, states[k + "/dims"], states[k + "/data"])
+    u = np.random.default_rng(40 + N).uniform(2, 10, N)
+    eng = Engine(L, p, Q, J, 0.01, 1e-8, 80, engine="hbm")
+    eng.set_states(st(50.0), st(2.5))
+    d1, F1 = _mid(eng, u, "0")
+    d2, F2 = _mid(eng, u, "1")
+    assert F1 == F2 and np.array_equal(d1, d2)
+    eng.close()
+
+
+def test_gradient_meet_in_the_middle_config4_vs_oracle():
+    """config 4's chain (Maxm 32): the meet-in-the-middle gradient == the stored
+    path bitwise and the oracle fixture's divT / F at the north_star tolerance"""
+    from optimalcontrolmps_amd.native import MPS, Engine
+    L, p, N, J, DT, CUT = 20, 7, 20, 1.0, 0.005, 1e-8
+    c4 = dict(np.load(os.path.join(HERE, "golden", "c4.npz"), allow_pickle=False))
+    u = c4["s32/u"]
+    eng = Engine(L, p, N, J, DT, CUT, int(c4["s32/maxm"]), engine="hbm")
+    eng.set_states(MPS(L, p, N, c4["s32/tgt_dims"], c4["s32/tgt_data"]),
+                   MPS(L, p, N, c4["s32/init_dims"], c4["s32/init_data"]))
+    d1, F1 = _mid(eng, u, "0")
+    d2, F2 = _mid(eng, u, "1")
+    assert F1 == F2 and np.array_equal(d1, d2)
+    assert np.abs(d2 - c4["s32/divT"]).max() <= 1e-8 * np.abs(c4["s32/divT"]).max()
+    g = DT * (d2 * F2 * 1j).real
+    assert np.abs(g - c4["s32/grad"]).max() <= 1e-6
+    eng.close()
