@@ -2796,16 +2796,92 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
     K = std::max(1, std::min(K, N - 1));
     const int S = (N - 1 + K - 1) / K;  // segments s = 0..S-1 cover [T_s, T_{s+1}], T_S = N - 1
     auto Tc = [&](int s) { return std::min(s * K, N - 1); };
-    // slots: 0 init, 1 target, then ckpsi[S+1], ckxi[S+1], segpsi[K+1], segxi[K+1], segxiH[K+1]
-    const int ckp = 2, ckx = ckp + S + 1, sgp = ckx + S + 1, sgx = sgp + K + 1, sgh = sgx + K + 1;
-    E.reserve_states(size_t(sgh + K + 1));
+    // slots: 0 init, 1 target, then ckpsi[S+1], ckxi[S+1], and a region that holds
+    // first the meet-in-the-middle half trajectories (N slots, when they fit) and
+    // then segpsi[K+1], segxi[K+1], segxiH[K+1]
+    const int ckp = 2, ckx = ckp + S + 1, R = ckx + S + 1, sgp = R, sgx = sgp + K + 1, sgh = sgx + K + 1;
     h->have_psi = h->have_xi = h->have_xih = false;  // the trajectory slots are overwritten
     h->N = 0;
+    // divT everywhere and F: psi || xi meeting in the middle (hbm_gradient_mid,
+    // every checkpoint stored on the way) when N half-trajectory slots fit, so the
+    // row passes recompute only the segments their rows need; else the
+    // checkpoint-only pass and divT in the first row pass
+    bool mid = false;
+    if (const char* e = std::getenv("OCG_HBM_CKPT_MID")) mid = std::atoi(e) != 0;
+    else mid = true;
+    if (mid) {
+      try {
+        E.reserve_states(size_t(R) + std::max<size_t>(size_t(N), size_t(3) * (K + 1)));
+      } catch (const hbm::Error& e) {
+        if (e.code != 6) throw;
+        (void)hipGetLastError();
+        mid = false;
+      }
+    }
+    E.reserve_states(size_t(sgh + K + 1));
     const double dt2 = E.dt * E.dt;
     Timer tall(h, 5);
-    // 1. psi forward / xi backward in one batch, checkpoints only
+    std::vector<std::complex<double>> dv(N, 0.0);
+    std::complex<double> Fc;
     E.reserve_chains(std::max(E.nchain_cap, 2), false);
-    {
+    auto ckpt_psi = [&](int t) { return (t == N - 1 || t % K == 0) ? ckp + (t == N - 1 ? S : t / K) : -1; };
+    auto ckpt_xi = [&](int t) { return (t == N - 1 || t % K == 0) ? ckx + (t == N - 1 ? S : t / K) : -1; };
+    if (mid) {
+      const int tm = (N - 1) / 2;
+      auto half = [&](int t) { return R + t; };  // psi_t for t <= tm, xi_t above
+      Chain* cp = E.acquire(false);
+      Chain* cx = E.acquire(false);
+      std::vector<Chain*> both{cp, cx};
+      E.load_many(both, {E.states[0].view(), E.states[1].view()});
+      E.store_many({&E.states[half(0)], &E.states[ckp], &E.states[half(N - 1)], &E.states[ckx + S]}, {cp, cp, cx, cx});
+      auto advance = [&](int& tp, int pe, int& tx, int xe) {
+        std::vector<Chain*> c;
+        std::vector<double> uf, ut;
+        std::vector<int> fw;
+        if (tp < pe) { c.push_back(cp); uf.push_back(u[tp]); ut.push_back(u[tp + 1]); fw.push_back(1); }
+        if (tx > xe) { c.push_back(cx); uf.push_back(u[tx]); ut.push_back(u[tx - 1]); fw.push_back(0); }
+        E.step(c, uf, ut, fw);
+        if (tp < pe) ++tp;
+        if (tx > xe) --tx;
+      };
+      int tp = 0, tx = N - 1;
+      while (tp < tm || tx > tm + 1) {  // phase 1: both halves stored, checkpoints on the way
+        const bool mp = tp < tm, mx = tx > tm + 1;
+        advance(tp, tm, tx, tm + 1);
+        std::vector<State*> ss;
+        std::vector<Chain*> cc;
+        if (mp) {
+          ss.push_back(&E.states[half(tp)]); cc.push_back(cp);
+          if (ckpt_psi(tp) >= 0) { ss.push_back(&E.states[ckpt_psi(tp)]); cc.push_back(cp); }
+        }
+        if (mx) {
+          ss.push_back(&E.states[half(tx)]); cc.push_back(cx);
+          if (ckpt_xi(tx) >= 0) { ss.push_back(&E.states[ckpt_xi(tx)]); cc.push_back(cx); }
+        }
+        E.store_many(ss, cc);
+      }
+      while (tp < N - 1 || tx > 0) {  // phase 2: each new state paired with the stored other half
+        const bool mp = tp < N - 1, mx = tx > 0;
+        advance(tp, N - 1, tx, 0);
+        std::vector<State*> ss;
+        std::vector<Chain*> cc;
+        if (mp && ckpt_psi(tp) >= 0) { ss.push_back(&E.states[ckpt_psi(tp)]); cc.push_back(cp); }
+        if (mx && ckpt_xi(tx) >= 0) { ss.push_back(&E.states[ckpt_xi(tx)]); cc.push_back(cx); }
+        if (!ss.empty()) E.store_many(ss, cc);
+        std::vector<View> xs, ys;  // divT_t = overlapC(xi_t, dH, psi_t) (:409-419)
+        if (mp) { xs.push_back(E.states[half(tp)].view()); ys.push_back(cp->view()); }
+        if (mx) { xs.push_back(cx->view()); ys.push_back(E.states[half(tx)].view()); }
+        const auto r = E.overlaps(xs, ys, true);
+        int k = 0;
+        if (mp) dv[tp] = r[k++];
+        if (mx) dv[tx] = r[k++];
+      }
+      Fc = E.overlaps({cp->view()}, {E.states[1].view()}, false)[0];  // F = overlapC(psi_{N-1}, target) (:242)
+      E.sync();
+      E.release(cp);
+      E.release(cx);
+    } else {
+      // 1. psi forward / xi backward in one batch, checkpoints only
       std::vector<Chain*> cs{E.acquire(false), E.acquire(false)};
       E.load_many(cs, {E.states[0].view(), E.states[1].view()});
       E.store_many({&E.states[ckp], &E.states[ckx + S]}, cs);
@@ -2818,18 +2894,17 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
         const int tp = s + 1, tx = N - 2 - s;
         std::vector<State*> ss;
         std::vector<Chain*> cc;
-        if (tp == N - 1 || tp % K == 0) { ss.push_back(&E.states[ckp + (tp == N - 1 ? S : tp / K)]); cc.push_back(cs[0]); }
+        if (ckpt_psi(tp) >= 0) { ss.push_back(&E.states[ckpt_psi(tp)]); cc.push_back(cs[0]); }
         if (tx % K == 0) { ss.push_back(&E.states[ckx + tx / K]); cc.push_back(cs[1]); }
         if (!ss.empty()) E.store_many(ss, cc);
       }
       E.sync();
       for (auto* c : cs) E.release(c);
+      // F = overlapC(psi_{N-1}, target) (:242)
+      Fc = E.overlaps({E.states[ckp + S].view()}, {E.states[1].view()}, false)[0];
     }
-    // F = overlapC(psi_{N-1}, target) (:242)
-    const std::complex<double> Fc = E.overlaps({E.states[ckp + S].view()}, {E.states[1].view()}, false)[0];
     F[0] = Fc.real();
     F[1] = Fc.imag();
-    std::vector<std::complex<double>> dv(N, 0.0);
     // 2. row batches (ascending rows; the first pass also forms divT everywhere)
     std::vector<int> rs(rows, rows + nrows);
     std::sort(rs.begin(), rs.end());
@@ -2837,7 +2912,7 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
     // in flight at once: the batch's row chains, a segment's xiH outputs (<= K)
     // and the two recomputation chains
     E.reserve_chains(std::max(E.nchain_cap, B + K + 2), false);
-    bool first = true;
+    bool first = !mid;  // without the middle pass the first row pass also forms divT
     for (int r0 = 0; first || r0 < nrows; r0 += B) {
       const int nb = std::min(B, nrows - r0);
       const int imin = nb > 0 ? rs[r0] : N;

@@ -24,16 +24,22 @@ def stored(eng, u, rows):
     return eng.hessian_rows(u, rows, F, divT), divT, F
 
 
-def ckpt(eng, u, rows, K):
+def ckpt(eng, u, rows, K, mid="1"):
     os.environ["OCG_HBM_CKPT"] = str(K)
+    os.environ["OCG_HBM_CKPT_MID"] = mid
     try:
         return eng.hessian(u, rows)
     finally:
         del os.environ["OCG_HBM_CKPT"]
+        del os.environ["OCG_HBM_CKPT_MID"]
 
 
+@pytest.mark.parametrize("mid", ["1", "0"])
 @pytest.mark.parametrize("K", [1, 3, 8])
-def test_ckpt_config1_states_bitwise(states, K):
+def test_ckpt_config1_states_bitwise(states, K, mid):
+    """mid "1": divT / F from psi || xi meeting in the middle (checkpoints stored on
+    the way), row passes recompute only their segments; "0": the checkpoint-only
+    pass, divT in the first row pass"""
     from optimalcontrolmps_amd.native import MPS, Engine
     L, p, N, J = 5, 5, 5, 1.0
 
@@ -45,12 +51,12 @@ def test_ckpt_config1_states_bitwise(states, K):
     eng = Engine(L, p, N, J, 0.01, 1e-8, 80, engine="hbm")
     eng.set_states(st(50.0), st(2.5))
     H1, d1, F1 = stored(eng, u, rows)
-    H2, d2, F2 = ckpt(eng, u, rows, K)
+    H2, d2, F2 = ckpt(eng, u, rows, K, mid)
     assert F1 == F2 and np.array_equal(d1, d2)
     assert np.array_equal(H1, H2)
     # a row subset in two batches of the time-major sweep
     sub = [3, 4, 11, 17]
-    H3, _, _ = ckpt(eng, u, sub, K)
+    H3, _, _ = ckpt(eng, u, sub, K, mid)
     for i in sub:
         assert np.array_equal(H3[i, i:19], H1[i, i:19]) and np.array_equal(H3[i:19, i], H1[i:19, i])
 
