@@ -1,10 +1,6 @@
 import os
 import sys
 
-# one hardware queue per HIP stream (the pipelined HBM getHessian uses three;
-# HIP's default is 4 per process) -- set before anything initialises HIP
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 import numpy as np
 import pytest
 
