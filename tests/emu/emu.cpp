@@ -160,6 +160,7 @@ size_t emu_apply_dH(void* h, const int* dims, const double* x, int* od, double* 
   return get(e, 3, od, ox);
 }
 
+#ifndef EMU_STEPS_ONLY  // the sanitizer build (tests/test_sanitizers.py) runs steps only
 void emu_overlap(void* h, const int* dx, const double* x, const int* dy, const double* y, int with_dH,
                  double* out) {
   Emu& e = *static_cast<Emu*>(h);
@@ -374,3 +375,6 @@ extern "C" void emu_decompose_multi(void* h, int nb, const int* Rs, const int* C
     c.sync();
   });
 }
+#else
+}  // extern "C" (closed inside the excluded part otherwise)
+#endif  // EMU_STEPS_ONLY

@@ -21,7 +21,8 @@ def lib():
         L.emu_free.argtypes = [C.c_void_p]
         L.emu_steps.restype = C.c_size_t
         L.emu_steps.argtypes = [C.c_void_p, ip, dp, dp, C.c_int, C.c_int, ip, dp]
-        L.emu_hessian_fused.argtypes = [C.c_void_p, ip, dp, ip, dp, dp, C.c_int, dp, dp, dp]
+        if hasattr(L, "emu_hessian_fused"):  # absent from the steps-only sanitizer build
+            L.emu_hessian_fused.argtypes = [C.c_void_p, ip, dp, ip, dp, dp, C.c_int, dp, dp, dp]
         _lib = L
     return _lib
 
