@@ -84,6 +84,7 @@ __device__ OCG_INLINE void body_trajectory(char* smem, OcgParams P, const zc* gf
   int t = fwd ? 0 : N - 1;
   if (fast_on(P)) {
     FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+    __syncthreads();  // load_tables' writes first: the region may alias them (P.fast_off = 0)
     f.init(P.fplan, gf, gb);
     f.load(SLOT_D(pool, P, src), SLOT_X(pool, P, src));
     f.store(SLOT_D(pool, P, base + t), SLOT_X(pool, P, base + t));
@@ -286,7 +287,12 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
   double bytes = 0, flops = 0, nsteps = 0;
   const bool fo = fast_on(P);
   FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
-  if (fo && (b < 2 || b >= 2 + nxw)) f.init(P.fplan, gf, gb);
+  // (the region may alias the general chain's LDS, P.fast_off = 0: a row worker
+  // initialises it only after its exactApplyMPO, below)
+  if (fo && b < 2) {
+    __syncthreads();  // load_tables' writes first (uniform: b is the workgroup's role)
+    f.init(P.fplan, gf, gb);
+  }
   if (b < 2 && fo) {
     // calcPsi / calcXi on the one-wave chain: every state stored write-through;
     // state t's flag is raised after step t+1 has been computed, when its
@@ -352,8 +358,10 @@ __device__ OCG_INLINE void body_pipeline(char* smem, OcgParams P, const zc* gf, 
     if (threadIdx.x == 0) rnorm0[(size_t)kc * nrows + r] = sqrt(n2);
     int k = kc * rbase[nrows] + rbase[r];  // control kc's row states follow control kc-1's
     c.store(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
-    if (fo) {  // the row's steps on the one-wave chain, from the general chain's LDS copy
-      f.load(flat(c.DIMS), flat(c.A));
+    if (fo) {  // the row's steps on the one-wave chain, from the stored psiH_i
+      __syncthreads();  // every wave's stores of psiH_i before the one-wave chain reads them
+      f.init(P.fplan, gf, gb);
+      f.load(SLOT_D(rs, P, k), SLOT_X(rs, P, k));
       for (int j = i + 1; j + 1 < N; ++j) {
         f.step(u[j - 1], u[j], 1, false);
         ++k;
@@ -435,6 +443,7 @@ __device__ OCG_INLINE void body_steps(char* smem, OcgParams P, const zc* gf, con
   const double* ui = u + (size_t)i * u_stride;
   if (fast_on(P)) {
     FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+    __syncthreads();  // load_tables' writes first: the region may alias them (P.fast_off = 0)
     f.init(P.fplan, gf, gb);
     f.load(SLOT_D(pool, P, slots[i]), SLOT_X(pool, P, slots[i]));
     for (int s = 0; s < nsteps; ++s) f.step(ui[s], ui[s + 1], forward);

@@ -175,9 +175,22 @@ struct ocg_ctx {
   // chain parameter block sized for two chain workgroups per CU (plan slots
   // shrunk to half the LDS, or none): many concurrent chains (ocg_hessian_multi)
   int plan_pe2 = 0, lds2 = 0;
+  // the one-wave chain's region aliasing the general chain's LDS (fast_off 0, the
+  // larger of the two sizes): for kernels whose workgroups use the general chain
+  // only before the one-wave chain starts (k_trajectory, k_steps, k_pipeline);
+  // k_hessian_rows hands states back and forth and keeps the two regions apart
+  int lds_alias = 0;
+  OcgParams Pa() const {
+    OcgParams q = P;
+    if (P.fplan && lds_alias > 0) {
+      q.fast_off = 0;
+      q.lds_bytes = lds_alias;
+    }
+    return q;
+  }
   OcgParams P2() const {
     OcgParams q = P;
-    if (P.fplan) return q;  // the one-wave chain's region follows the plan-less layout (one chain per CU)
+    if (P.fplan) return Pa();  // the one-wave chain: aliased regions (two or more chains per CU)
     if (plan_pe2 >= 32) {
       q.plan_pe = plan_pe2;
       q.lds_bytes = lds2;
@@ -546,6 +559,13 @@ static int finish_params(ocg_ctx* c) {
   c->P.lds_bytes = off + fbytes;
   c->plan_pe2 = 0;
   c->lds2 = 0;
+#ifdef OCG_PROFILE
+  c->lds_alias = 0;  // the diagnostic build's phase counters live in the general chain's LDS
+#else
+  c->lds_alias = std::max(l.bytes, fbytes);
+  if (const char* e = std::getenv("OCG_FAST_ALIAS"))
+    if (e[0] == '0') c->lds_alias = 0;
+#endif
   return 0;
 }
 
@@ -784,7 +804,8 @@ static int launch_steps(ocg_ctx* c, int slot, const double* u, int nsteps, int f
   HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * (nsteps + 1), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_idx, &slot, sizeof(int), hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_steps, dim3(1), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+  const OcgParams Pa = c->Pa();  // the one-wave chain aliases the general LDS
+  hipLaunchKernelGGL(k_steps, dim3(1), dim3(NT), Pa.lds_bytes, c->stream, Pa, c->d_gf, c->d_gb, c->d_md, c->pool,
                      c->d_idx, 1, c->d_u, nsteps + 1, nsteps, forward, c->d_stats + 4 * 3);
   return end_kernel(c, 4);
 }
@@ -947,7 +968,8 @@ int ocg_step_batch(ocg_ctx* c, int n, const int* dims, const double* const* data
   HIPCHK(c, hipMemcpyAsync(c->d_u, uu.data(), sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_idx, slots.data(), sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_steps, dim3(n), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md, c->pool,
+  const OcgParams Pa = c->Pa();  // the one-wave chain aliases the general LDS
+  hipLaunchKernelGGL(k_steps, dim3(n), dim3(NT), Pa.lds_bytes, c->stream, Pa, c->d_gf, c->d_gb, c->d_md, c->pool,
                      c->d_idx, n, c->d_u, 2, 1, forward, c->d_stats + 4 * 3);
   if (int rc = end_kernel(c, 4)) return rc;
   for (int i = 0; i < n; ++i)
@@ -1060,7 +1082,8 @@ int ocg_propagate(ocg_ctx* c, const double* u, int N, int which) {
   HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * N, hipMemcpyHostToDevice, c->stream));
   int grid = (which == 3) ? 2 : 1;
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_trajectory, dim3(grid), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+  const OcgParams Pa = c->Pa();  // the one-wave chain aliases the general LDS
+  hipLaunchKernelGGL(k_trajectory, dim3(grid), dim3(NT), Pa.lds_bytes, c->stream, Pa, c->d_gf, c->d_gb, c->d_md,
                      c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->d_u, N, which,
                      c->d_stats + 0 * 3, 0);
   if (int rc = end_kernel(c, 0)) return rc;
@@ -1150,7 +1173,8 @@ int ocg_gradient_multi(ocg_ctx* c, int K, const double* u, int N, double* divT, 
   if (int rc = ensure_buf(c, c->d_u, c->u_cap, K * N)) return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_u, u, sizeof(double) * K * N, hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  hipLaunchKernelGGL(k_trajectory, dim3(2 * K), dim3(NT), P.lds_bytes, c->stream, P, c->d_gf, c->d_gb, c->d_md,
+  const OcgParams Pa = c->Pa();  // the one-wave chain aliases the general LDS
+  hipLaunchKernelGGL(k_trajectory, dim3(2 * K), dim3(NT), Pa.lds_bytes, c->stream, Pa, c->d_gf, c->d_gb, c->d_md,
                      c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(), c->d_u, N, 3,
                      c->d_stats + 0 * 3, cs);
   if (int rc = end_kernel(c, 0)) return rc;
@@ -1507,7 +1531,7 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
     const char* e = std::getenv("OCG_MULTI_SHARE_K");
     return e ? std::atoi(e) : 8;
   }();
-  const OcgParams Pl = (share_k > 0 && K >= share_k) ? c->P2() : P;
+  const OcgParams Pl = (share_k > 0 && K >= share_k) ? c->P2() : c->Pa();
   hipLaunchKernelGGL(k_pipeline, dim3(K * (2 + nxw + nrows)), dim3(NT), Pl.lds_bytes, c->stream, Pl, c->d_gf,
                      c->d_gb, c->d_md, c->pool, c->slot_init(), c->slot_target(), c->psi_base(), c->xi_base(),
                      c->xih_base(), c->d_u, N, d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_flags, epoch, c->d_err,

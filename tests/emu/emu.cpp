@@ -142,6 +142,7 @@ size_t emu_steps(void* h, const int* dims, const double* x, const double* u, int
   put(e, 2, dims, x);
   int slot = 2;
   OcgParams P = e.P;
+  P.fast_off = 0;  // as ocg_steps: the one-wave chain's region aliases the general chain's LDS
   launch(e, 1, [&](char* smem) {
     ocg::body_steps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), &slot, 1, u, nsteps + 1, nsteps, fwd,
                         e.stats + 12);
@@ -258,8 +259,10 @@ void emu_hessian_fused(void* h, const int* dt_, const double* tgt, const int* di
   std::vector<int> flags(2 * N + 3, 0);
   int err = 0;
   const int nxw = N < 8 ? N : 8;
+  OcgParams PA = P;
+  PA.fast_off = 0;  // as ocg_hessian: aliased regions in k_pipeline
   launch(e, 2 + nxw + nrows, [&](char* smem) {
-    ocg::body_pipeline<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, xih, u, N, rows.data(),
+    ocg::body_pipeline<NT>(smem, PA, e.GF(), e.GB(), e.md.data(), e.pool(), 0, 1, psi, xi, xih, u, N, rows.data(),
                            nrows, rb.data(), rs, rn.data(), flags.data(), 1, &err, nxw, e.stats, 1, 0);
   });
   std::vector<int> xs(N), ys(N);
