@@ -439,9 +439,16 @@ struct FastChain {
       const int bi = side == 0 ? tho + (i < n ? i : 0) * C : tho + (i < n ? i : 0);
       const int bj = side == 0 ? tho + (j < n ? j : 0) * C : tho + (j < n ? j : 0);
       const int len1 = lane < no1 ? o1[1] : 0, b1 = o1[0], s1 = o1[2];
-      if (dot <= 4) gram_dots<4>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
-      else if (dot <= 8) gram_dots<8>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
-      else gram_dots<kMaxDot>(M, len, st, bi, bj, len1, b1, s1, gv, lam1);
+      switch ((dot + 1) >> 1) {  // unrolled to the even bound above the op's longest dot
+        case 0: case 1: gram_dots<2>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        case 2: gram_dots<4>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        case 3: gram_dots<6>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        case 4: gram_dots<8>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        case 5: gram_dots<10>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        case 6: gram_dots<12>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        case 7: gram_dots<14>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+        default: gram_dots<kMaxDot>(M, len, st, bi, bj, len1, b1, s1, gv, lam1); break;
+      }
       if (side == 1) gv.y = -gv.y;
     }
     if (!valid) gv = c2(0.0, 0.0);
@@ -634,6 +641,39 @@ struct FastChain {
     }
   }
 
+  // The rotation of the pair this lane holds (CH::jrot_fast's formulas, the
+  // identity when !live), returned as this lane's role coefficients: index p
+  // (up): J[p][p] = c, J[q][p] = -s e*, shift -sh; index q: J[q][q] = c e*,
+  // J[p][q] = s, shift +sh.  The rare power-of-two rescale runs only when some
+  // lane needs it (sc = 1 otherwise: the same bits as without it).
+  __device__ __forceinline__ void jrot_role(zc bv, double app, double aqq, bool live, bool up, zc& jd, zc& jo,
+                                            double& ds) const {
+    const double mb = fmax(fabs(bv.x), fabs(bv.y)), sz = fabs(app) + fabs(aqq);
+    const bool resc = live && (mb < 1e-120 || mb > 1e120 || sz > 1e120);
+    double sc = 1.0;
+    if (__ballot(resc)) {
+      sc = resc ? ldexp(1.0, -ilogb(fmax(mb, sz))) : 1.0;
+      bv = cscale(bv, sc);
+      app *= sc;
+      aqq *= sc;
+    }
+    const double r2 = live ? bv.x * bv.x + bv.y * bv.y : 1.0;
+    const double rinv = CH::rsq_ref(r2), r = r2 * rinv;
+    const double D = aqq - app, sg = D >= 0 ? 1.0 : -1.0;
+    const double x = fma(D, D, 4.0 * r2);
+    const double E = fabs(D) + x * CH::rsq_ref(x);
+    const double h = CH::rsq_ref(fma(E, E, 4.0 * r2));
+    const double c = E * h, s = sg * 2.0 * r * h;
+    const double ex = bv.x * rinv, ey = bv.y * rinv;
+    const double sh = sg * 2.0 * r2 * CH::rcp_ref(E * sc);
+    jd = up ? c2(c, 0.0) : c2(ex * c, -ey * c);
+    jo = up ? c2(ex * -s, -ey * -s) : c2(s, 0.0);
+    ds = up ? -sh : sh;
+    jd = live ? jd : c2(1.0, 0.0);
+    jo = live ? jo : c2(0.0, 0.0);
+    ds = live ? ds : 0.0;
+  }
+
   // register Jacobi on up to four Gram blocks of order <= 4 (Chain::jacobi_reg<4>):
   // lane 16 g + 4 i + j holds G[i][j] and W[i][j] of group g; round r pairs
   // x with x ^ (r + 1), partner elements by DPP, rotations by bpermute.  The
@@ -681,16 +721,9 @@ struct FastChain {
         const zc bv = up ? g : g11;  // the pivot element g[p][q] (for the mirror: its DPP partner)
         const double app = up ? di : dj, aqq = up ? dj : di;
         const bool need = CH::jneed(cabs2(bv), app, aqq);
-        zc cs, e;
-        double sh;
-        CH::jrot_fast(bv, app, aqq, need, cs, e, sh);
-        const zc ec = cconj(e);
-        zc jd = up ? c2(cs.x, 0.0) : cscale(ec, cs.x);   // p: c,        q: c e*
-        zc jo = up ? cscale(ec, -cs.y) : c2(cs.y, 0.0);  // p: -s e*,    q: s
-        double ds = up ? -sh : sh;                        // p: -shift,   q: +shift
-        jd = dg ? c2(1.0, 0.0) : jd;
-        jo = dg ? c2(0.0, 0.0) : jo;
-        ds = dg ? 0.0 : ds;
+        zc jd, jo;
+        double ds;
+        jrot_role(bv, app, aqq, need && !dg, up, jd, jo, ds);
         const zc jdc = CH::bpermz(jd, acol[rnd]), joc = CH::bpermz(jo, acol[rnd]);
         const zc jdr = CH::bpermz(jd, arow[rnd]), jor = CH::bpermz(jo, arow[rnd]);
         const double dsc = CH::bperm(ds, acol[rnd]), dsr = CH::bperm(ds, arow[rnd]);
