@@ -125,3 +125,37 @@ def test_gradient_meet_in_the_middle_config4_vs_oracle():
     g = DT * (d2 * F2 * 1j).real
     assert np.abs(g - c4["s32/grad"]).max() <= 1e-6
     eng.close()
+
+
+@pytest.mark.parametrize("engine", ["hbm", "lds"])
+def test_ocg_gradient_vs_oracle_config1(states, engine):
+    """ocg_gradient against the CPU oracle (not a path equality): config 1's chain,
+    N_t = 41, divT to 1e-8 of its scale, F to 1e-9, the GRAPE gradient to the
+    north_star 1e-6 -- through the meet-in-the-middle path on the HBM engine and
+    the stored trajectories on the LDS engine (the one-wave chain)"""
+    import oracle_ffi as O
+    from optimalcontrolmps_amd.native import MPS, Engine
+    L, p, Q, J, DT = 5, 5, 5, 1.0, 0.01
+
+    def st(U):
+        k = state_key(L, p, Q, J, U)
+        return states[k + "/dims"], states[k + "/data"]
+    (dt_, xt), (di, xi) = st(50.0), st(2.5)
+    N = 41
+    u = np.random.default_rng(77).uniform(2, 10, N)
+    oc = O.OC(O.Stepper(L, p, Q, J, DT, 1e-8, 80), O.MPS(L, p, Q, dt_, xt), O.MPS(L, p, Q, di, xi), N, 0.0)
+    go = oc.gradient(u)
+    do, Fo = oc.divT_F()
+    if engine == "hbm":
+        os.environ["OCG_HBM_MID"] = "1"
+    try:
+        eng = Engine(L, p, Q, J, DT, 1e-8, 80, engine=engine)
+        eng.set_states(MPS(L, p, Q, dt_, xt), MPS(L, p, Q, di, xi))
+        d, F = eng.gradient(u)
+        eng.close()
+    finally:
+        os.environ.pop("OCG_HBM_MID", None)
+    assert abs(F - Fo) <= 1e-9
+    assert np.abs(d - do).max() <= 1e-8 * np.abs(do).max()
+    g = DT * (d * F * 1j).real
+    assert np.abs(g - go).max() <= 1e-6
