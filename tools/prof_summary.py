@@ -95,5 +95,62 @@ def main(tag, outdir=None):
         print(r)
 
 
+def one_pass(kind, tag, out):
+    """one pass of a long command per GPU call (each under the call's time limit):
+    its partial summary (kernel stats, or one counter's per-kernel sums) as JSON"""
+    d = db(kind, tag)
+    if kind == "prof":
+        res = {"kernels": kernel_stats(d)}
+    else:
+        counter = {"pmc_fetch": "FETCH_SIZE", "pmc_write": "WRITE_SIZE"}[kind]
+        res = {"counter": counter, "sums": pmc(d, counter)}
+    with open(out, "w") as f:
+        json.dump(res, f)
+
+
+def merge(tag, parts, outdir=None):
+    """profiles/<tag>_{kernel_stats.csv,pmc.csv,summary.json} from one_pass outputs"""
+    prof = outdir or os.path.join(ROOT, "profiles")
+    ks, fetch, write = [], {}, {}
+    for pth in parts:
+        with open(pth) as f:
+            r = json.load(f)
+        if "kernels" in r:
+            ks = r["kernels"]
+        elif r["counter"] == "FETCH_SIZE":
+            fetch = r["sums"]
+        else:
+            write = r["sums"]
+    with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["kernel", "calls", "total_ms", "avg_ms", "pct"])
+        w.writeheader()
+        for r in ks:
+            w.writerow(r)
+    per = {}
+    with open(os.path.join(prof, f"{tag}_pmc.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "dispatches", "FETCH_SIZE_KB_per_dispatch", "WRITE_SIZE_KB_per_dispatch",
+                    "hbm_bytes_per_dispatch_corrected"])
+        for k in sorted(set(fetch) | set(write)):
+            fk = fetch.get(k, [0.0, 1])
+            wk = write.get(k, [0.0, 1])
+            f_kb, w_kb = fk[0] / fk[1], wk[0] / wk[1]
+            corrected = 2.0 * f_kb * 1024 + w_kb * 1024
+            per[k] = dict(dispatches=fk[1], fetch_kb=f_kb, write_kb=w_kb, hbm_bytes=corrected)
+            w.writerow([k, fk[1], f"{f_kb:.3f}", f"{w_kb:.3f}", f"{corrected:.0f}"])
+    summary = dict(tag=tag, kernels=ks, pmc_per_dispatch=per, pmc_issue={},
+                   note="rocprofv3 --kernel-trace --stats and separate --pmc passes (FETCH_SIZE, WRITE_SIZE) of "
+                        "the same `python3 bench.py` command, each pass in a GPU call of its own (one pass "
+                        "nearly fills a call's time limit); FETCH_SIZE doubled per the gfx950 calibration")
+    with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: v for k, v in per.items() if "gemm" in k}, indent=1))
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else None)
+    if len(sys.argv) > 1 and sys.argv[1] == "--pass":
+        one_pass(sys.argv[2], sys.argv[3], sys.argv[4])
+    elif len(sys.argv) > 1 and sys.argv[1] == "--merge":
+        merge(sys.argv[2], sys.argv[3:])
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else None)
