@@ -32,7 +32,7 @@ static inline zc mkz(double x, double y) { zc r; r.x = x; r.y = y; return r; }
 #define OCG_NT 128
 #endif
 static constexpr int NT = OCG_NT;
-static constexpr int kXiHWorkers = 8;
+static constexpr int kXiHWorkers = 12;  // A/B (config 1, one-wave chain): 8 -> 7.62 ms, 12 -> 7.53, 16 -> 7.53, 24 -> 7.49 per pipeline
 
 #include "kernels.hpp"
 using ocg::Pool;
@@ -1524,7 +1524,12 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   HIPCHK(c, hipEventRecord(c->evh[0], c->stream));
   // xiH workers: the xi chain publishes one state per step and one dH
   // application costs about one step, so a few workers keep up
-  const int nxw = std::min(N, kXiHWorkers);
+  static const int xiw = [] {  // A/B: OCG_XIH_WORKERS
+    const char* e = std::getenv("OCG_XIH_WORKERS");
+    const int v = e ? std::atoi(e) : kXiHWorkers;
+    return v > 0 ? v : kXiHWorkers;
+  }();
+  const int nxw = std::min(N, xiw);
   // many controls: chain workgroups sized for two per CU (smaller plan slots; plans are
   // bitwise-neutral) — measured 37.3k vs 33.0k rows/s at K = 8, slower below (OCG_MULTI_SHARE_K)
   static const int share_k = [] {
