@@ -1375,6 +1375,13 @@ struct Chain {
       }
     }
     sync();
+#ifdef OCG_FAST_TRACE  // CPU emulation diagnostics: block orders of decompositions beyond the register Jacobi
+    if (tid == 0 && ISCAL[I_MAXROUNDS] > 7) {
+      printf("[lds-jacobi] orders");
+      for (int q = 0; q < Q1; ++q) printf(" %d", NQ[q]);
+      printf("\n");
+    }
+#endif
     pf(2);
     // Gram matrices and identity eigenvectors (on a plan hit with blocks of
     // order 2..8 the register Jacobi forms them itself)
