@@ -348,6 +348,28 @@ def test_hessian_multi_equals_single(states, K, Nt):
             assert np.array_equal(fid_m, eng.fidelities())
 
 
+def test_hessian_multi_vs_oracle(states):
+    """ocg_hessian_multi (one-wave chains, aliased LDS, two chains per CU) against
+    the CPU oracle rather than against itself: three controls at N_t = 31, every
+    Hessian to the north_star 1e-6 of its scale, divT and F to 1e-8 / 1e-9"""
+    L, p, N, J, dt = 5, 5, 5, 1.0, 0.01
+    Nt, K = 31, 3
+    U = np.random.default_rng(505).uniform(2, 10, (K, Nt))
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+    eng = engine(L, p, N, J, dt, 1e-8, 80)
+    eng.set_states(tgt, ini)
+    Hm, dm, Fm = eng.hessian_multi(U)
+    eng.close()
+    st = O.Stepper(L, p, N, J, dt, 1e-8, 80)
+    for k in range(K):
+        oc = O.OC(st, O.MPS(L, p, N, tgt.dims, tgt.data), O.MPS(L, p, N, ini.dims, ini.data), Nt, 0.0)
+        Ho = oc.hessian(U[k], 4)
+        do, Fo = oc.divT_F()
+        assert abs(Fm[k] - Fo) <= 1e-9, k
+        assert np.abs(dm[k] - do).max() <= 1e-8 * np.abs(do).max(), k
+        assert np.abs(Hm[k] - Ho).max() <= 1e-6 * np.abs(Ho).max(), k
+
+
 def test_hessian_multi_shared_cu_layout_bitwise(states, monkeypatch):
     """K >= OCG_MULTI_SHARE_K runs the chains with the two-per-CU LDS layout
     (smaller plan slots): the same Hessians bit for bit"""
