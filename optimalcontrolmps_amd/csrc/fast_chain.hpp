@@ -800,6 +800,23 @@ struct FastChain {
     wsync();
   }
 
+  // sin / cos of |x| <= pi/4 by their Taylor series through x^17 / x^16 (the
+  // next terms are below 1e-17): the step's phase arguments |u dt n(n-1)/4| are
+  // far inside that for the controls of the reference's drivers; larger ones take
+  // libm's sincos (uniform branch in step)
+  __device__ __forceinline__ static void sincos_q(double x, double& s, double& c) {
+    constexpr double s3 = -1.0 / 6.0, s5 = 1.0 / 120.0, s7 = -1.0 / 5040.0, s9 = 1.0 / 362880.0,
+                     s11 = -1.0 / 39916800.0, s13 = 1.0 / 6227020800.0, s15 = -1.0 / 1307674368000.0,
+                     s17 = 1.0 / 355687428096000.0;
+    constexpr double c2_ = -0.5, c4 = 1.0 / 24.0, c6 = -1.0 / 720.0, c8 = 1.0 / 40320.0, c10 = -1.0 / 3628800.0,
+                     c12 = 1.0 / 479001600.0, c14 = -1.0 / 87178291200.0, c16 = 1.0 / 20922789888000.0;
+    const double z = x * x;
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, s17, s15), s13), s11), s9), s7), s5), s3);
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, fma(z, c16, c14), c12), c10), c8), c6), c4), c2_);
+    s = fma(x * z, ps, x);
+    c = fma(z, pc, 1.0);
+  }
+
   // ------------------------------------------------------------- step
   // BH_tDMRG::step (src/BH_tDMRG.cpp:111-125) + doStep (:127-230), as Chain::step
   // (final_gauge = false: the closing position(1) is skipped, the centre stays on
@@ -810,28 +827,40 @@ struct FastChain {
     pf(29);
     const int p = P.p;
     const double tau = forward ? P.dt : -P.dt;
-    if (lane < p) {  // U phases exp(-i u tau n(n-1) / 4) (initUGates, :74-108)
-      const double nn = double(lane) * double(lane - 1);
-      double s, c;
-      zc f;
-      if (ufrom == ph_u && forward == ph_dir) {
-        f = PH[p + lane];
+    // U phases exp(-i u tau n(n-1) / 4) (initUGates, :74-108): lane < p the
+    // single-site UF[n], UT[n]; lane < p^2 the pair products UF[n1] UF[n2],
+    // UT[a1] UT[a2] as the phase of the summed argument -- all in registers, one
+    // LDS write and one wave fence
+    {
+      const double ta = -0.25 * tau;
+      const int a = lane / p, b = lane - a * p;
+      const double n1 = lane < p ? double(lane) * double(lane - 1) : 0.0;
+      const double n2 = lane < p * p ? double(a) * double(a - 1) + double(b) * double(b - 1) : 0.0;
+      const double xf1 = ta * ufrom * n1, xt1 = ta * uto * n1, xf2 = ta * ufrom * n2, xt2 = ta * uto * n2;
+      const bool big = fmax(fmax(fabs(xf1), fabs(xt1)), fmax(fabs(xf2), fabs(xt2))) > 0.78;
+      double sf1, cf1, st1, ct1, sf2, cf2, st2, ct2;
+      if (__ballot(big) == 0) {
+        sincos_q(xf1, sf1, cf1);
+        sincos_q(xt1, st1, ct1);
+        sincos_q(xf2, sf2, cf2);
+        sincos_q(xt2, st2, ct2);
       } else {
-        sincos(-0.25 * ufrom * tau * nn, &s, &c);
-        f = c2(c, s);
+        sincos(xf1, &sf1, &cf1);
+        sincos(xt1, &st1, &ct1);
+        sincos(xf2, &sf2, &cf2);
+        sincos(xt2, &st2, &ct2);
       }
-      PH[lane] = f;
-      sincos(-0.25 * uto * tau * nn, &s, &c);
-      PH[p + lane] = c2(c, s);
+      if (lane < p) {
+        PH[lane] = c2(cf1, sf1);
+        PH[p + lane] = c2(ct1, st1);
+      }
+      if (lane < p * p) {
+        PH[2 * p + lane] = c2(cf2, sf2);
+        PH[2 * p + p * p + lane] = c2(ct2, st2);
+      }
     }
     ph_u = uto;
     ph_dir = forward;
-    wsync();
-    for (int x = lane; x < p * p; x += 64) {  // pair products UF[n1] UF[n2], UT[a1] UT[a2]
-      const int a = x / p, b = x - a * p;
-      PH[2 * p + x] = cmul(PH[a], PH[b]);
-      PH[2 * p + p * p + x] = cmul(PH[p + a], PH[p + b]);
-    }
     wsync();
     for (int o = 0; o < nops; ++o) {
       const LDS int* oh = PL + PL[kHOps + o];
