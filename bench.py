@@ -717,7 +717,7 @@ def bench_c4(args):
         t_sc = time.perf_counter() - t_sc
     steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
     row_steps = R * (R - 1) // 2   # row i steps from i to N_t-2
-    paths = eng.stats(8)
+    paths = eng.path_stats()
     reps = 1 if strong else world   # independent Hessians / gradients per step
     sweep = args.steps * (steps_traj * (world if (strong or grad) else reps) + (0 if grad else row_steps * reps))
     gemm_ms = gm["ms"] / max(1, gm["launches"])
@@ -767,9 +767,9 @@ def bench_c4(args):
                                                "k_gemm launches are small (tasks of m, n ~ 16-60) and latency-bound"),
         }
         if not grad:
-            res["hessian_path"] = {"pipelined": paths["launches"], "pipeline_fallbacks": paths["sweep_steps"],
-                                   "checkpointed": int(paths["alg_flops"]),
-                                   "checkpoint_segment": int(paths["alg_bytes"]) or None}
+            res["hessian_path"] = {"pipelined": paths["pipe_runs"], "pipeline_fallbacks": paths["pipe_fallbacks"],
+                                   "checkpointed": paths["ckpt_runs"],
+                                   "checkpoint_segment": paths["ckpt_k"] or None}
         res["env"] = run_env()
         if world == 1 and not args.no_cpu_baseline and not grad and not args.profiled:
             res["cpu_baseline"] = (cpu_baseline_c5(ini, Nt, args.cpu_threads) if c5 else

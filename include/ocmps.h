@@ -71,7 +71,18 @@ int ocg_device_count(int* n);
 int ocg_destroy(ocg_ctx* ctx);
 /* last error message of ctx (or of the last failed ocg_create when ctx == NULL) */
 const char* ocg_last_error(const ocg_ctx* ctx);
+/* writes sizeof(ocg_info) bytes of the header the library was built with
+ * (ABI version 3: fast_chain is the last field); callers built against
+ * another version use ocg_get_info_sz */
 int ocg_get_info(const ocg_ctx* ctx, ocg_info* info);
+/* as ocg_get_info, writing at most info_size bytes (the caller's sizeof(ocg_info)) */
+int ocg_get_info_sz(const ocg_ctx* ctx, ocg_info* info, size_t info_size);
+/* ABI version of the library (OCG_ABI_VERSION of the header it was built with).
+ * Changelog: 2 ocg_info.fast_chain (round 5), OCG_ENOMEM returned by
+ * ocg_hessian when OCG_HBM_PIPE=1 forces a pipeline that cannot allocate;
+ * 3 ocg_get_info_sz, ocg_get_path_stats, ocg_abi_version (round 6). */
+#define OCG_ABI_VERSION 3
+int ocg_abi_version(void);
 /* BH_tDMRG::setTstep (src/BH_tDMRG.cpp:61-65) */
 int ocg_set_tstep(ocg_ctx* ctx, double tstep);
 /* number of complex elements of an MPS with the given dims */
@@ -237,6 +248,22 @@ int ocg_denmat_decomp(ocg_ctx* ctx, int nm, const int* rows, const int* cols, co
 int ocg_kernel_stats(ocg_ctx* ctx, int kind, double* total_ms, long* launches, double* alg_bytes,
                      double* alg_flops, long* sweep_steps);
 int ocg_reset_stats(ocg_ctx* ctx);
+/* Which paths the HBM engine's calls took since the context was created (named
+ * counters; ocg_kernel_stats kind 8 returns the first four through its timing
+ * fields and stays for old callers).  The caller sets out->size =
+ * sizeof(ocg_path_stats); only that many bytes are written.  Zeros on the LDS
+ * engine. */
+typedef struct ocg_path_stats {
+  size_t size;           /* set by the caller: sizeof(ocg_path_stats) of its header */
+  long pipe_runs;        /* pipelined getHessians completed */
+  long pipe_fallbacks;   /* two-phase reruns after a pipeline that failed with OCG_ENOMEM */
+  long ckpt_runs;        /* trajectory-checkpointed getHessians completed */
+  long ckpt_k;           /* segment length of the last checkpointed getHessian */
+  long coop_launches;    /* multi-CU eigenvalue launches (k_heev_vals_coop) */
+  long coop_groups;      /* Gram blocks reduced by a group of workgroups */
+  long coop_fallbacks;   /* of those, groups that gave up a wait and were re-run on one CU */
+} ocg_path_stats;
+int ocg_get_path_stats(ocg_ctx* ctx, ocg_path_stats* out);
 /* diagnostic builds (-DOCG_PROFILE) only: shader-clock cycles per engine phase
  * (32 slots, see engine_device.hpp Chain::pf), summed over workgroups; zeros in
  * the product build.  reset != 0 clears after reading. */

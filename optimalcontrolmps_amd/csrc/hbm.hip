@@ -226,6 +226,24 @@ struct Engine {
   // smallest Gram order on the blocked kernel k_heev_vals_big (default: the orders the register
   // kernels cannot hold); OCG_HBM_BIGMIN overrides (tests; > kBigMax: the eager L2 kernel, A/B)
   int big_min = std::getenv("OCG_HBM_BIGMIN") ? std::atoi(std::getenv("OCG_HBM_BIGMIN")) : RNMAX + 1;
+  // Gram orders coop_min..CPT on the multi-CU reduction k_heev_vals_coop (hbm_coop.hpp), G
+  // workgroups per block, G picked per launch from the CUs the launch's blocks leave (results do
+  // not depend on G).  OCG_HBM_COOP=0: off (the one-CU kernels above); OCG_HBM_COOPMIN=n: the
+  // smallest order; OCG_HBM_COOPG=g: fixed G (A/B, tests); OCG_HBM_COOP_TMO: the bound on every
+  // wait in s_memrealtime ticks (100 MHz; a group that gives up is re-run on one CU)
+  bool coop_on = !(std::getenv("OCG_HBM_COOP") && std::getenv("OCG_HBM_COOP")[0] == '0');
+  int coop_min = std::getenv("OCG_HBM_COOPMIN") ? std::atoi(std::getenv("OCG_HBM_COOPMIN")) : RNMAX + 1;
+  int coop_g = std::getenv("OCG_HBM_COOPG") ? std::atoi(std::getenv("OCG_HBM_COOPG")) : 0;
+  long long coop_tmo = std::getenv("OCG_HBM_COOP_TMO") ? std::atoll(std::getenv("OCG_HBM_COOP_TMO")) : 20000000LL;
+  int n_cu = 256;
+  DBuf<int> coop_fb;  // [0]: groups re-run on one CU (k_heev_vals_coop_fix), read by path_stats
+  long coop_launches = 0, coop_groups = 0;
+  // workgroups per block for a launch of nb blocks whose largest order is nmax
+  int coop_members(int nb, int nmax) const {
+    if (coop_g > 0) return std::min(coop_g, kCoopMaxG);
+    const int gmax = std::max(1, std::min(8, nmax / 64));
+    return std::max(1, std::min(gmax, n_cu / std::max(nb, 1)));
+  }
   // Maxm-boundary eigenvalue resolution (k_heev_thresh + k_heev_bisect) for
   // register-path Gram blocks of order >= thresh_min; OCG_HBM_THRESH=1: on,
   // OCG_HBM_THRESH=n > 1: on from order n.  Off by default: at config 4 the two
@@ -320,6 +338,12 @@ struct Engine {
     HCK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     HCK(hipEventCreateWithFlags(&ev_kept, hipEventDisableTiming));
+    {
+      int ncu = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) n_cu = ncu;
+      coop_fb.reserve(1);
+      HCK(hipMemsetAsync(coop_fb.p, 0, sizeof(int), st));  // ordered before every side-stream launch (ev_fork)
+    }
     {
       std::vector<z> I(size_t(kCholMax) * kCholMax, mk(0, 0));
       for (int i = 0; i < kCholMax; ++i) I[size_t(i) * kCholMax + i] = mk(1, 0);
@@ -914,10 +938,11 @@ struct Engine {
       // kernel), largest blocks first; dynamic LDS = max over the variants present
       // orders big_min <= n <= kBigMax: the blocked reduction (k_heev_vals_big)
       // orders <= kSmallMax: k_heev_vals_small on the side stream (several workgroups per CU)
-      std::vector<int> order, big, small;
+      std::vector<int> order, big, small, coop;
       for (int i = 0; i < np; ++i) {
         const int n = R.probs[i].n;
-        if (n >= std::max(big_min, 2) && n <= kBigMax) big.push_back(i);
+        if (coop_on && n >= std::max(coop_min, 65) && n <= CPT) coop.push_back(i);
+        else if (n >= std::max(big_min, 2) && n <= kBigMax) big.push_back(i);
         else if (small_split && n <= kSmallMax) small.push_back(i);
         else order.push_back(i);
       }
@@ -926,12 +951,26 @@ struct Engine {
       if (gstat)
         for (int i = 0; i < np; ++i) ++eig_hist[std::min(R.probs[i].n / 16, 33)];
       std::stable_sort(big.begin(), big.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
-      const bool side = !big.empty() || !small.empty();
+      std::stable_sort(coop.begin(), coop.end(), [&](int a, int b) { return R.probs[a].n > R.probs[b].n; });
+      const bool side = !big.empty() || !small.empty() || !coop.empty();
       if (side) {  // on the side stream, after everything st has queued (incl. this upload)
         const int* dbig = upload(big);
         const int* dsmall = upload(small);
+        const int* dcoop = upload(coop);
+        int* dctl = coop.empty() ? nullptr : walloc<int>(size_t(kCoopCtl) * coop.size());
         HCK(hipEventRecord(ev_fork, st));
         HCK(hipStreamWaitEvent(st2, ev_fork, 0));
+        if (!coop.empty()) {
+          // largest blocks first in dispatch order; every group's control words zeroed
+          const int nc = int(coop.size()), G = coop_members(nc, R.probs[coop[0]].n);
+          HCK(hipMemsetAsync(dctl, 0, sizeof(int) * kCoopCtl * nc, st2));
+          hipLaunchKernelGGL(k_heev_vals_coop, dim3(8 * G * ((nc + 7) / 8)), dim3(CPT), 0, st2, R.d_probs, dcoop, nc,
+                             G, dctl, coop_tmo);
+          hipLaunchKernelGGL(k_heev_vals_coop_fix, dim3(nc), dim3(VBG), 0, st2, R.d_probs, dcoop,
+                             (const int*)dctl, coop_fb.p);
+          ++coop_launches;
+          coop_groups += nc;
+        }
         if (!big.empty())
           hipLaunchKernelGGL(k_heev_vals_big, dim3(int(big.size())), dim3(VBG), 0, st2, R.d_probs, dbig);
         if (!small.empty()) {
@@ -3045,6 +3084,26 @@ int hbm_stats(hbm_engine* h, int kind, double* ms, long* launches, double* bytes
   if (flops) *flops = 0;
   if (steps) *steps = h->steps[kind];
   return 0;
+}
+int hbm_coop_stats(hbm_engine* h, long* launches, long* groups, long* fallbacks) {
+  long l = 0, g = 0, f = 0;
+  const int rc = guard(h, [&] {
+    for (hbm::Engine* X : {h->E.get(), h->W[0].get(), h->W[1].get()}) {
+      if (!X) continue;
+      l += X->coop_launches;
+      g += X->coop_groups;
+      if (X->coop_fb.p) {
+        int v = 0;
+        HCK(hipStreamSynchronize(X->st2));
+        HCK(hipMemcpy(&v, X->coop_fb.p, sizeof(int), hipMemcpyDeviceToHost));
+        f += v;
+      }
+    }
+  });
+  if (launches) *launches = l;
+  if (groups) *groups = g;
+  if (fallbacks) *fallbacks = f;
+  return rc;
 }
 void hbm_reset_stats(hbm_engine* h) {
   for (int k = 0; k < 8; ++k) { h->ms[k] = 0; h->launches[k] = 0; h->steps[k] = 0; }

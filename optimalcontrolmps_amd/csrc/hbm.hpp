@@ -62,6 +62,9 @@ int hbm_get_state(hbm_engine* h, int which, int t, int* dims, double* data, size
 // kinds 0-6 as ocg_kernel_stats (HIP-event phase times); 7: the MFMA GEMM
 // kernel (k_gemm) with its algorithmic bytes and flops
 int hbm_stats(hbm_engine* h, int kind, double* ms, long* launches, double* bytes, double* flops, long* steps);
+// multi-CU eigenvalue launches, blocks reduced by groups, groups re-run on one CU
+// (the context engine and the pipelined getHessian's workers, since creation)
+int hbm_coop_stats(hbm_engine* h, long* launches, long* groups, long* fallbacks);
 void hbm_reset_stats(hbm_engine* h);
 bool hbm_have(const hbm_engine* h, int what);  // 0 states, 1 psi, 2 xi, 3 xiH
 int hbm_N(const hbm_engine* h);

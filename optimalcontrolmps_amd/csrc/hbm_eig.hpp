@@ -1424,7 +1424,7 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
 constexpr int VBG = 512;
 constexpr int kBigMax = VBG;  // one row per thread
 constexpr int BNB = 12;
-__global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__ probs, const int* __restrict__ idx) {
+__device__ __forceinline__ void vals_big_body(const EProb& P) {
   constexpr int NWV = VBG / 64;
   __shared__ z LU[kBigMax], LP[kBigMax], LB[kBigMax];
   __shared__ double Ld[kBigMax], Le2[kBigMax];
@@ -1432,7 +1432,6 @@ __global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__
   __shared__ double red[NWV], scal[4];
   __shared__ __align__(16) z ws[8 * kBigMax];  // product partials [8][kBigMax] | panel staging [4][64][BNB]
   static_assert(4 * 64 * BNB <= 8 * kBigMax, "panel staging fits the partials region");
-  const EProb P = probs[idx[blockIdx.x]];
   const int n = P.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (n < 2 || n > kBigMax) return;
   z* A = P.A;
@@ -1670,5 +1669,10 @@ __global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__
            stamp_acc[0], stamp_acc[1], stamp_acc[2], stamp_acc[3], stamp_acc[4], stamp_acc[5], stamp_acc[6]);
 #endif
 }
+__global__ __launch_bounds__(VBG) void k_heev_vals_big(const EProb* __restrict__ probs, const int* __restrict__ idx) {
+  vals_big_body(probs[idx[blockIdx.x]]);
+}
 
 }  // namespace hbm
+
+#include "hbm_coop.hpp"

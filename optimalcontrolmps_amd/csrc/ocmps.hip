@@ -759,6 +759,35 @@ int ocg_destroy(ocg_ctx* c) {
   return 0;
 }
 
+int ocg_abi_version(void) { return OCG_ABI_VERSION; }
+
+int ocg_get_info_sz(const ocg_ctx* c, ocg_info* info, size_t info_size) {
+  if (!c || !info) return OCG_EINVAL;
+  ocg_info full{};
+  const int rc = ocg_get_info(c, &full);
+  if (rc) return rc;
+  std::memcpy(info, &full, std::min(info_size, sizeof(full)));
+  return 0;
+}
+
+int ocg_get_path_stats(ocg_ctx* c, ocg_path_stats* out) {
+  if (!c || !out || out->size < sizeof(size_t)) return OCG_EINVAL;
+  ocg_path_stats v{};
+  v.size = sizeof(v);
+  v.pipe_runs = c->pipe_runs;
+  v.pipe_fallbacks = c->pipe_fallbacks;
+  v.ckpt_runs = c->ckpt_runs;
+  v.ckpt_k = c->ckpt_k;
+  if (c->hbm) {
+    const int rc = hbm_coop_stats(c->hbm, &v.coop_launches, &v.coop_groups, &v.coop_fallbacks);
+    if (rc) return hb(c, rc);
+  }
+  const size_t sz = std::min(out->size, sizeof(v));
+  std::memcpy(out, &v, sz);
+  out->size = sz;
+  return 0;
+}
+
 int ocg_get_info(const ocg_ctx* c, ocg_info* info) {
   if (!c || !info) return OCG_EINVAL;
   if (c->hbm) {

@@ -83,6 +83,12 @@ class OcgInfo(C.Structure):
                 ("lds_bytes", C.c_int), ("block_threads", C.c_int), ("device", C.c_int), ("fast_chain", C.c_int)]
 
 
+class OcgPathStats(C.Structure):
+    _fields_ = [("size", C.c_size_t), ("pipe_runs", C.c_long), ("pipe_fallbacks", C.c_long),
+                ("ckpt_runs", C.c_long), ("ckpt_k", C.c_long), ("coop_launches", C.c_long),
+                ("coop_groups", C.c_long), ("coop_fallbacks", C.c_long)]
+
+
 # (name, restype, argtypes) for every entry point of include/ocmps.h
 SIGNATURES = [
     ("ocg_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
@@ -93,6 +99,9 @@ SIGNATURES = [
     ("ocg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("ocg_last_error", C.c_char_p, [C.c_void_p]),
     ("ocg_get_info", C.c_int, [C.c_void_p, C.POINTER(OcgInfo)]),
+    ("ocg_get_info_sz", C.c_int, [C.c_void_p, C.POINTER(OcgInfo), C.c_size_t]),
+    ("ocg_abi_version", C.c_int, []),
+    ("ocg_get_path_stats", C.c_int, [C.c_void_p, C.POINTER(OcgPathStats)]),
     ("ocg_set_tstep", C.c_int, [C.c_void_p, C.c_double]),
     ("ocg_mps_nelem", C.c_size_t, [C.c_int, C.c_int, C.c_int, ip]),
     ("ocg_step", C.c_int, [C.c_void_p, ip, dp, C.c_double, C.c_double, C.c_int, ip, dp, C.c_size_t, szp]),
@@ -442,6 +451,15 @@ class Engine:
                                          C.byref(s)), "ocg_kernel_stats")
         return {"ms": ms.value, "launches": n.value, "alg_bytes": b.value, "alg_flops": f.value,
                 "sweep_steps": s.value}
+
+    def path_stats(self):
+        """named path counters of the HBM engine (ocg_get_path_stats): pipelined /
+        two-phase-fallback / checkpointed getHessians, multi-CU eigenvalue launches,
+        blocks and groups re-run on one CU"""
+        st = OcgPathStats()
+        st.size = C.sizeof(OcgPathStats)
+        self._chk(lib().ocg_get_path_stats(self.h, C.byref(st)), "ocg_get_path_stats")
+        return {k: getattr(st, k) for k, _ in OcgPathStats._fields_ if k != "size"}
 
     def profile(self, reset=True):
         out = np.zeros(32)

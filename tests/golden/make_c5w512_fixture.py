@@ -11,7 +11,13 @@ Writes tests/golden/c5_w512.npz.  Run: python tests/golden/make_c5w512_fixture.p
 `... make_c5w512_fixture.py hess`: from that state (psi_init = psi_target =
 the saturated state, so no second state is stored), N_t = 5 GRAPE controls
 U(2,10) (seed 5512): divT, F, gradient and the full fidelity Hessian on the
-oracle with 8 threads -> tests/golden/c5_w512h.npz."""
+oracle with 8 threads -> tests/golden/c5_w512h.npz.
+
+`... make_c5w512_fixture.py hess9`: psi_init = the saturated state, psi_target
+= that state stepped three times by the oracle at U = 4.0 (so psi_init !=
+psi_target and both sit at chi = 512), N_t = 9 GRAPE controls U(2,10) (seed
+5519): divT, F, gradient and the full fidelity Hessian (7 rows of up to 6 row
+steps) -> tests/golden/c5_w512h9.npz (the target state stored with it)."""
 import os
 import sys
 import time
@@ -44,9 +50,33 @@ def make_hess():
     np.savez_compressed(os.path.join(HERE, "c5_w512h.npz"), u=u, H=H, grad=g, divT=divT, F=np.array([F]))
 
 
+def make_hess9(threads=6):
+    z = np.load(os.path.join(HERE, "c5_w512.npz"), allow_pickle=False)
+    st = O.Stepper(L, p, N, J, DT, CUT, MAXM)
+    psi = O.MPS(L, p, N, z["dims"], z["data"])
+    t0 = time.time()
+    tgt = st.steps(psi, np.array([2.5, 4.0, 4.0, 4.0]), True)
+    print(f"w512h9 target {time.time() - t0:.1f}s bonds {list(tgt.bond_dims())}", flush=True)
+    Nt = 9
+    u = np.random.default_rng(5519).uniform(2.0, 10.0, Nt)
+    oc = O.OC(st, tgt, psi, Nt, 0.0)
+    t0 = time.time()
+    H = oc.hessian(u, threads)
+    secs = time.time() - t0
+    divT, F = oc.divT_F()
+    g = DT * (divT * F * 1j).real
+    print(f"w512h9 oracle hessian {secs:.1f}s on {threads} threads max|H| {np.abs(H).max():.3e} "
+          f"max|g| {np.abs(g).max():.3e} F {F}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "c5_w512h9.npz"), u=u, H=H, grad=g, divT=divT, F=np.array([F]),
+                        tdims=tgt.dims, tdata=tgt.data, secs=np.array([secs]), threads=np.array([threads]))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["hess"]:
         make_hess()
+        sys.exit(0)
+    if sys.argv[1:2] == ["hess9"]:
+        make_hess9(int(sys.argv[2]) if len(sys.argv) > 2 else 6)
         sys.exit(0)
     st = O.Stepper(L, p, N, J, DT, CUT, MAXM)
     if os.path.exists(CKPT):

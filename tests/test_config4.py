@@ -269,7 +269,7 @@ def test_c4_s32_pipelined_equals_stored(c4, monkeypatch):
         full = e.hessian(u)
         shard = e.hessian(u + 1e-3, zigzag_rows(Nt - 2, 1, 3))
         # the path really taken: two pipelined calls (no two-phase retry) or none
-        assert e.stats(8)["launches"] == (2 if mode == "1" else 0) and e.stats(8)["sweep_steps"] == 0
+        assert e.path_stats()["pipe_runs"] == (2 if mode == "1" else 0) and e.path_stats()["pipe_fallbacks"] == 0
         fid = e.fidelities()
         xih = e.state(2, 3)
         out[mode] = (full, shard, fid, xih)
@@ -296,7 +296,7 @@ def test_c4_w256_hessian_vs_oracle(c4, warm256, monkeypatch, pipe):
     eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
     eng.set_states(_mps(c4["w256h/tgt_dims"], c4["w256h/tgt_data"]), warm256)
     H, divT, F = eng.hessian(u)
-    assert eng.stats(8)["launches"] == (1 if pipe == "1" else 0) and eng.stats(8)["sweep_steps"] == 0
+    assert eng.path_stats()["pipe_runs"] == (1 if pipe == "1" else 0) and eng.path_stats()["pipe_fallbacks"] == 0
     g = DT * (divT * F * 1j).real
     Fo, go, Ho = complex(c4["w256h/F"][0]), c4["w256h/grad"], c4["w256h/H"]
     assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12
@@ -328,7 +328,7 @@ def test_c4_w256_hessian_long_vs_oracle(c4, warm256, monkeypatch, pipe, path):
     eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
     eng.set_states(_mps(c4["w256h/tgt_dims"], c4["w256h/tgt_data"]), warm256)
     H, divT, F = eng.hessian(z["u"])
-    assert eng.stats(8)["launches"] == (1 if pipe == "1" else 0) and eng.stats(8)["sweep_steps"] == 0
+    assert eng.path_stats()["pipe_runs"] == (1 if pipe == "1" else 0) and eng.path_stats()["pipe_fallbacks"] == 0
     g = DT * (divT * F * 1j).real
     Fo = complex(z["F"][0])
     assert abs(F - Fo) <= 1e-9 * abs(Fo) + 1e-12

@@ -99,6 +99,8 @@ def test_trajectories_gradient_hessian_vs_golden(states, oracle_golden, case):
     name, (L, p, N, J), Ui, Uf, dt, cut, maxm = case
     u = oracle_golden[name + "/u"]
     eng = engine(L, p, N, J, dt, cut, maxm)
+    if name == "config1":  # config 1 runs on the one-wave padded chain (csrc/fast_chain.hpp)
+        assert eng.info.fast_chain == 1
     divT, F, fid, H = run_engine_hessian(eng, u, st_of(states, L, p, N, J, Uf), st_of(states, L, p, N, J, Ui))
     assert np.abs(divT - oracle_golden[name + "/divT"]).max() < 1e-9
     assert abs(F - oracle_golden[name + "/F"][0]) < 1e-9
@@ -174,6 +176,8 @@ def test_fused_hessian_vs_golden(states, oracle_golden, case):
     name, (L, p, N, J), Ui, Uf, dt, cut, maxm = case
     u = oracle_golden[name + "/u"]
     eng = engine(L, p, N, J, dt, cut, maxm)
+    if name == "config1":  # the headline path: the one-wave padded chain, not the general one
+        assert eng.info.fast_chain == 1
     eng.set_states(st_of(states, L, p, N, J, Uf), st_of(states, L, p, N, J, Ui))
     H, divT, F = eng.hessian(u)
     assert np.abs(divT - oracle_golden[name + "/divT"]).max() < 1e-9

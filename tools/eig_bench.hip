@@ -26,6 +26,7 @@ int main(int argc, char** argv) {
   std::normal_distribution<double> N01;
   std::vector<std::vector<cd>> As(B);
   for (int b = 0; b < B; ++b) {
+    if (b > 0 && getenv("EIG_SAME")) { As[b] = As[0]; continue; }  // every problem the same block
     std::vector<cd> M(size_t(n) * n), A(size_t(n) * n);
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) M[i * n + j] = j < rank ? cd(N01(g), N01(g)) * std::exp(-0.08 * j) : cd(0, 0);
@@ -74,13 +75,24 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dbt, sizeof(int2) * bt.size()));
     CK(hipMemcpy(dbt, bt.data(), sizeof(int2) * bt.size(), hipMemcpyHostToDevice));
   }
+  // EIG_COOP=G: the multi-CU kernel with G workgroups per block (EIG_TMO: its
+  // wait bound in s_memrealtime ticks; 0 forces every group onto the fallback)
+  const int coopG = getenv("EIG_COOP") ? atoi(getenv("EIG_COOP")) : 0;
+  const long long coop_tmo = getenv("EIG_TMO") ? atoll(getenv("EIG_TMO")) : 5000000LL;
+  int* dctl = nullptr;
+  CK(hipMalloc(&dctl, sizeof(int) * kCoopCtl * B));
   hipEvent_t e0, e1, e2;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2));
   double tv = 0, tvec = 0;
   for (int rep = 0; rep < reps; ++rep) {
     for (int b = 0; b < B; ++b) CK(hipMemcpy(dA + nn * b, As[b].data(), sizeof(z) * nn, hipMemcpyHostToDevice));
     CK(hipEventRecord(e0));
-    if (n > RNMAX && n <= kBigMax && !getenv("EIG_OLD")) {
+    if (coopG > 0) {
+      CK(hipMemsetAsync(dctl, 0, sizeof(int) * kCoopCtl * B, 0));
+      hipLaunchKernelGGL(k_heev_vals_coop, dim3(8 * coopG * ((B + 7) / 8)), dim3(CPT), 0, 0, dP, didx, B, coopG, dctl,
+                         coop_tmo);
+      hipLaunchKernelGGL(k_heev_vals_coop_fix, dim3(B), dim3(VBG), 0, 0, dP, didx, dctl, nullptr);
+    } else if (n > RNMAX && n <= kBigMax && !getenv("EIG_OLD")) {
       hipLaunchKernelGGL(k_heev_vals_big, dim3(B), dim3(VBG), 0, 0, dP, didx);
     } else {
       const int lds = (n >= regmin && n <= RNMAX) ? reg_lds_bytes(reg_grid(n)) : 64 * n + (n <= kLdsOrder ? 16 * n * n : 0) + 64;
@@ -142,6 +154,27 @@ int main(int argc, char** argv) {
     printf("\n");
   }
 #endif
+  if (coopG > 0) {
+    std::vector<int> ctl(kCoopCtl * B);
+    CK(hipMemcpy(ctl.data(), dctl, sizeof(int) * ctl.size(), hipMemcpyDeviceToHost));
+    int ab = 0;
+    for (int b = 0; b < B; ++b) ab += ctl[kCoopCtl * b + 32] != 0;
+    printf("coop G=%d: %d of %d groups fell back | ", coopG, ab, B);
+  }
+  // eigenvalues of every problem vs problem 0's (the same matrix in every slot)
+  {
+    std::vector<double> wa(size_t(n) * B);
+    CK(hipMemcpy(wa.data(), dw, 8 * n * B, hipMemcpyDeviceToHost));
+    double dmax = 0;
+    for (int b = 1; b < B; ++b)
+      for (int i = 0; i < n; ++i) dmax = std::max(dmax, std::abs(wa[size_t(b) * n + i] - wa[i]));
+    if (getenv("EIG_DUMPW")) {
+      FILE* f = fopen(getenv("EIG_DUMPW"), "wb");
+      fwrite(wa.data(), 8, n, f);
+      fclose(f);
+    }
+    printf("max|w_b - w_0| %.2e | ", dmax);
+  }
   printf("n=%d B=%d k=%d: vals %.1f us  vecs %.1f us per launch | max|A u - w u|/w0 = %.2e  orth %.2e  "
          "trace err %.2e  w0 %.3e w[k-1] %.3e\n", n, B, kk, 1e3 * tv / (reps - 1), 1e3 * tvec / (reps - 1),
          res / w[0], orth, std::abs(tr - sw) / tr, w[0], w[kk - 1]);
