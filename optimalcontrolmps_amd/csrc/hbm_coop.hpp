@@ -1,6 +1,7 @@
 // Multi-CU Hermitian eigenvalue stage of the HBM engine: one Gram block of
-// order 64 < n <= 512 (config 4's sectors of order 128-208, config 5's of
-// order 209-512 at chi = 512) reduced by a GROUP of G workgroups on G CUs.
+// order 64 < n <= 512 (by default the orders 209-512 the one-CU register
+// kernels cannot hold: config 5's sectors at chi = 512) reduced by a GROUP of
+// G workgroups on G CUs.
 //
 // The reference's truncation (ITensor denmatDecomp, src/BH_tDMRG.cpp:178,
 // 191,209) diagonalises rho = Θ Θ^H per U(1) sector.  On one CU
@@ -58,6 +59,9 @@ constexpr int CNB = 12;       // panel width
 constexpr int CMB = 8;        // own 16-column blocks per matvec pass
 constexpr int kCoopCtl = 64;  // ints of control words per group: counter at 0, abort word at 32
 constexpr int kCoopMaxG = 16;
+#ifndef COOP_MODEA_MIN
+#define COOP_MODEA_MIN 24  // own 16-column blocks from which each wave sums whole column groups itself
+#endif
 
 // global-address-space views: the hand-off's loads and stores must be
 // global_ (not flat_) sc1 instructions (MI355X_MICROARCH.md, Consumer bullet)
@@ -148,32 +152,101 @@ __device__ __forceinline__ int sturm_count1(const double* d, const double* e2, i
   return c;
 }
 
-// 48 doubles per lane -> the wave's sums, 3 per 4-lane group: lane L holds
-// sums [b, b + 3), b = 24 b5 + 12 b4 + 6 b3 + 3 b2 (b_k = bit k of L), the
-// same in the 4 lanes of the group; a fixed order (identical in every member).
-// The first halving step (xor 32) is done by the caller as the values are
-// formed (value i and 24 + i together), so only 24 live here.
-__device__ __forceinline__ double rs_first(double lo24, double hi24, int lane) {
-  const bool up = (lane & 32) != 0;
-  const double keep = up ? hi24 : lo24, send = up ? lo24 : hi24;
-  return keep + __shfl_xor(send, 32, 64);
+// cross-lane moves of a double without LDS: DPP within rows of 16 lanes, the
+// gfx950 permlane swaps across rows / halves
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
 }
-__device__ __forceinline__ void wave_reduce_scatter24(double (&v)[24], int lane) {
+__device__ __forceinline__ double join_d(unsigned lo, unsigned hi) {
+  return __longlong_as_double((long long)lo | ((long long)hi << 32));
+}
+// a' = [a lanes 0-31 | b lanes 0-31], b' = [a lanes 32-63 | b lanes 32-63]:
+// lane L < 32 sees (a[L], a[L + 32]), lane L >= 32 sees (b[L - 32], b[L])
+__device__ __forceinline__ void swap32(double& a, double& b) {
+#ifdef COOP_DBG_NOSWAP
+  { const double pa = __shfl_xor(a, 32, 64), pb = __shfl_xor(b, 32, 64); const bool up = (threadIdx.x & 32) != 0; const double na = up ? pb : a, nb = up ? b : pa; a = na; b = nb; return; }
+#endif
+  const long long ia = __double_as_longlong(a), ib = __double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane32_swap(unsigned(ia), unsigned(ib), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(unsigned(ia >> 32), unsigned(ib >> 32), false, false);
+  a = join_d(lo[0], hi[0]);
+  b = join_d(lo[1], hi[1]);
+}
+// the same between rows 0/1 and 2/3 (lane L and L ^ 16)
+__device__ __forceinline__ void swap16(double& a, double& b) {
+#ifdef COOP_DBG_NOSWAP
+  { const double pa = __shfl_xor(a, 16, 64), pb = __shfl_xor(b, 16, 64); const bool up = (threadIdx.x & 16) != 0; const double na = up ? pb : a, nb = up ? b : pa; a = na; b = nb; return; }
+#endif
+  const long long ia = __double_as_longlong(a), ib = __double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane16_swap(unsigned(ia), unsigned(ib), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(unsigned(ia >> 32), unsigned(ib >> 32), false, false);
+  a = join_d(lo[0], hi[0]);
+  b = join_d(lo[1], hi[1]);
+}
+// wave sum, the same bits in every lane (every pairwise step is commutative)
+__device__ __forceinline__ double wave_allsum(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror: the row's sum in its 16 lanes
+  double a = v, b = v;
+  swap16(a, b);
+  v = a + b;
+  a = v;
+  b = v;
+  swap32(a, b);
+  return a + b;
+}
+// reduce-scatter step: lanes with the step's bit clear keep the sum of value
+// lo, the others of value hi (each lane adds its partner's)
+__device__ __forceinline__ double rs32(double lo, double hi) {
+  swap32(lo, hi);
+  return lo + hi;
+}
+__device__ __forceinline__ double rs16(double lo, double hi) {
+  swap16(lo, hi);
+  return lo + hi;
+}
+__device__ __forceinline__ double rs8(double lo, double hi, int lane) {
+  const bool up = (lane & 8) != 0;
+  const double keep = up ? hi : lo, send = up ? lo : hi;
+  return keep + dpp_d<0x128>(send);  // row_ror:8 = lane ^ 8 within the row
+}
+// sum over the 8 lanes of a half-row, the same bits in all 8
+__device__ __forceinline__ double sum8(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  return v;
+}
+
+// conj(A[k][col]) u_k summed over the 32 rows of chunk c in row order (explicit
+// fma: the same bits wherever it is called; rows <= j and invalid columns are
+// zeros).  Loads in batches of 8 (one L2 round trip each).
+__device__ __forceinline__ z chunk_acc(const z* __restrict__ S, int n, int col, bool cok, int j, int c, z u0,
+                                       const z* LU) {
+  z acc = mk(0, 0);
+#pragma unroll 1
+  for (int hh = 0; hh < 4; ++hh) {
+    z av[8];
 #pragma unroll
-  for (int st = 1; st < 4; ++st) {
-    const int o = 32 >> st, h = 24 >> st;
-    const bool up = (lane & o) != 0;
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int k = 32 * c + 8 * hh + s8;
+      av[s8] = (cok && k > j && k < n) ? ldz_g(S + (size_t)k * n + col) : mk(0, 0);
+    }
 #pragma unroll
-    for (int i = 0; i < h; ++i) {
-      const double keep = up ? v[h + i] : v[i], send = up ? v[i] : v[h + i];
-      v[i] = keep + __shfl_xor(send, o, 64);
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int k = 32 * c + 8 * hh + s8;
+      const z uk = k == j + 1 ? u0 : LU[k];
+      acc.x = fma(av[s8].x, uk.x, fma(av[s8].y, uk.y, acc.x));
+      acc.y = fma(av[s8].x, uk.y, fma(-av[s8].y, uk.x, acc.y));
     }
   }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    v[i] += __shfl_xor(v[i], 2, 64);
-    v[i] += __shfl_xor(v[i], 1, 64);
-  }
+  return acc;
 }
 
 // grid: 8 * G * ceil(ngroup / 8) workgroups of CPT threads; block b is member
@@ -182,6 +255,9 @@ __device__ __forceinline__ void wave_reduce_scatter24(double (&v)[24], int lane)
 __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restrict__ probs,
                                                            const int* __restrict__ idx, int ngroup, int G,
                                                            int* __restrict__ ctl, long long tmo) {
+  // XCD-local groups: members at consecutive dispatch positions of one XCD
+  // (blocks b, b + 8, ...), which measured ~3 % faster than spreading a group
+  // over the XCDs (gi = b / G)
   const int bid = blockIdx.x, slot = bid >> 3, gi = (slot / G) * 8 + (bid & 7), me = slot - (slot / G) * G;
   if (gi >= ngroup) return;
   const EProb P = probs[idx[gi]];
@@ -211,11 +287,11 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
   if (tid < 4 * CNB) (&Nx[0][0][0])[tid] = mk(0, 0);
   __syncthreads();
   z pu[CNB], pw[CNB];
-  z ru = mk(0, 0), rw = mk(0, 0);
+  z ru = mk(0, 0), rw = mk(0, 0);  // row j's panel slot l - 1 (computed by every thread)
 #ifdef HBM_STAMP
   unsigned long long stamp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stamp_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
-#endif  // row j's panel slot l - 1 (computed by every thread)
+#endif
   int hop = 0;
   int panel = 0;
   const int nblk = (n + 15) >> 4;
@@ -224,16 +300,24 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
     const z* S = panel == 0 ? A0 : Ab;
 #pragma unroll
     for (int q = 0; q < CNB; ++q) { pu[q] = mk(0, 0); pw[q] = mk(0, 0); }
+    z xnext = mk(0, 0);  // the panel's first column
+    if (r >= p0 && r < n)
+      xnext = panel == 0 ? ldz_g(A0 + (size_t)r * n + p0) : ldz_sc1(xc + (size_t)((panel & 1) * CNB) * n + r);
     for (int j = p0; j < pe; ++j) {
       const int l = j - p0;
       // (a) column j with the panel's pending updates: x = A_j - U W^H - W U^H
-      z x = mk(0, 0);
+      // (its stored value was loaded during the previous column)
+      z x = xnext;
+      if (j + 1 < pe && r >= j + 1 && r < n)
+        xnext = panel == 0 ? ldz_g(A0 + (size_t)r * n + j + 1)
+                           : ldz_sc1(xc + (size_t)((panel & 1) * CNB + l + 1) * n + r);
       if (r >= j && r < n) {
-        x = panel == 0 ? ldz_g(A0 + (size_t)r * n + j) : ldz_sc1(xc + (size_t)((panel & 1) * CNB + l) * n + r);
 #pragma unroll
         for (int q = 0; q < CNB; ++q) {
-          const z rU = q == l - 1 ? ru : Nx[j & 1][0][q], rW = q == l - 1 ? rw : Nx[j & 1][1][q];
-          x = zsub(x, zadd(zmul(pu[q], zcj(rW)), zmul(pw[q], zcj(rU))));
+          if (q < l) {  // slots l.. are zero (uniform branch)
+            const z rU = q == l - 1 ? ru : Nx[j & 1][0][q], rW = q == l - 1 ? rw : Nx[j & 1][1][q];
+            x = zsub(x, zadd(zmul(pu[q], zcj(rW)), zmul(pw[q], zcj(rU))));
+          }
         }
       }
       if (r == j) Ld[j] = x.x;
@@ -243,9 +327,7 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
         for (int q = 0; q < CNB; ++q) { Nx[(j + 1) & 1][0][q] = pu[q]; Nx[(j + 1) & 1][1][q] = pw[q]; }
       }
       LU[r] = x;
-      double v = (r >= j + 2 && r < n) ? x.x * x.x + x.y * x.y : 0.0;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      const double v = wave_allsum((r >= j + 2 && r < n) ? x.x * x.x + x.y * x.y : 0.0);
       if (lane == 0) red1[wv] = v;
       __syncthreads();
       double s = 0;
@@ -280,42 +362,51 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
         const int k0 = cb_lo <= me ? 0 : (cb_lo - me + G - 1) / G;
         const int nown = me + G * k0 < nblk ? (nblk - 1 - me) / G - k0 + 1 : 0;
         const int c_lo = (j + 1) >> 5, nch = ((n - 1) >> 5) - c_lo + 1;
+        // this member's column p_i and the u^H A u partial of its block (lanes of one
+        // 16-lane row = one block), handed off with sc1 stores
+        auto finish = [&](z p, int cb, int i) {
+          const bool li = i > j && i < n;
+          const z ui = li ? (i == j + 1 ? u0 : LU[i]) : mk(0, 0);
+          z e = li ? zcjmul(ui, p) : mk(0, 0);
+          // the block's sum over its 16 lanes (one DPP row), the same bits in each
+          e.x += dpp_d<0xB1>(e.x); e.y += dpp_d<0xB1>(e.y);
+          e.x += dpp_d<0x4E>(e.x); e.y += dpp_d<0x4E>(e.y);
+          e.x += dpp_d<0x141>(e.x); e.y += dpp_d<0x141>(e.y);
+          e.x += dpp_d<0x140>(e.x); e.y += dpp_d<0x140>(e.y);
+          if (li) stz_sc1(pb + hb * n + i, p);
+          if ((i & 15) == 0) stz_sc1(bp + hb * 32 + cb, e);
+        };
+        if (nown >= COOP_MODEA_MIN) {
+          // every wave busy with whole 64-column groups: each lane sums its column's
+          // chunks in order itself (the same bits as the partials below)
+          for (int g4 = wv; 4 * g4 < nown; g4 += 8) {
+            const int bi = 4 * g4 + (lane >> 4), cb = me + G * (k0 + bi), col = 16 * cb + (lane & 15);
+            const bool cok = bi < nown && col > j && col < n;
+            z p = mk(0, 0);
+            for (int c = c_lo; c < c_lo + nch; ++c) {
+              const z acc = chunk_acc(S, n, col, cok, j, c, u0, LU);
+              p = c == c_lo ? acc : zadd(p, acc);
+            }
+            if (bi < nown) finish(p, cb, col);
+          }
+        } else
         for (int b0 = 0; b0 < nown; b0 += CMB) {
           const int nb = nown - b0 < CMB ? nown - b0 : CMB;
-          for (int it = wv; it < nb * nch; it += 8) {
-            const int bi = it % nb, c = c_lo + it / nb;
-            const int col = 16 * (me + G * (k0 + b0 + bi)) + (lane & 15), sub = lane >> 4;
-            const bool cok = col > j && col < n;
-            z av[8];
-#pragma unroll
-            for (int s8 = 0; s8 < 8; ++s8) {
-              const int k = 32 * c + sub + 4 * s8;
-              av[s8] = (cok && k > j && k < n) ? ldz_g(S + (size_t)k * n + col) : mk(0, 0);
-            }
-            z acc = mk(0, 0);
-#pragma unroll
-            for (int s8 = 0; s8 < 8; ++s8) {
-              const int k = 32 * c + sub + 4 * s8;
-              const z uk = k == j + 1 ? u0 : LU[k];
-              acc.x += av[s8].x * uk.x + av[s8].y * uk.y;
-              acc.y += av[s8].x * uk.y - av[s8].y * uk.x;
-            }
-            acc = zadd(acc, shfl_z(acc, 16));
-            acc = zadd(acc, shfl_z(acc, 32));
-            if (lane < 16) ws[(c - c_lo) * (CMB * 16) + bi * 16 + lane] = acc;
+          // items (64-column group, 32-row chunk): lane = column, the chunk's rows summed in order
+          const int ncg = (nb + 3) >> 2;
+          for (int it = wv; it < ncg * nch; it += 8) {
+            const int cgl = it % ncg, c = c_lo + it / ncg;
+            const int bi = cgl * 4 + (lane >> 4);
+            const int col = 16 * (me + G * (k0 + b0 + bi)) + (lane & 15);
+            const bool cok = bi < nb && col > j && col < n;
+            ws[(c - c_lo) * (CMB * 16) + cgl * 64 + lane] = chunk_acc(S, n, col, cok, j, c, u0, LU);
           }
           __syncthreads();
           if (tid < nb * 16) {
             const int cb = me + G * (k0 + b0 + (tid >> 4)), i = 16 * cb + (tid & 15);
             z p = ws[tid];
             for (int c = 1; c < nch; ++c) p = zadd(p, ws[c * (CMB * 16) + tid]);
-            const bool li = i > j && i < n;
-            const z ui = li ? (i == j + 1 ? u0 : LU[i]) : mk(0, 0);
-            z e = li ? zcjmul(ui, p) : mk(0, 0);
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) e = zadd(e, shfl_z(e, o));
-            if (li) stz_sc1(pb + hb * n + i, p);
-            if ((tid & 15) == 0) stz_sc1(bp + hb * 32 + cb, e);
+            finish(p, cb, i);
           }
           if (b0 + CMB < nown) __syncthreads();  // the partials are reused
         }
@@ -329,18 +420,31 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
       STAMP(3);
       // (d) dots W^H u, U^H u over rows j+1.. (while the other members finish)
       {
-        double dv[24];
+        // values 2q, 2q+1 (W_q^H u) and 24+2q, 24+2q+1 (U_q^H u): halved by xor 32,
+        // 16, 8 (permlane swaps, DPP), then summed over the remaining 8 lanes
+        double d24[24];
 #pragma unroll
         for (int q = 0; q < CNB; ++q) {
-          const z a1 = zcjmul(pw[q], ur), b1 = zcjmul(pu[q], ur);  // values 2q, 2q+1 | 24+2q, 24+2q+1
-          dv[2 * q] = rs_first(a1.x, b1.x, lane);
-          dv[2 * q + 1] = rs_first(a1.y, b1.y, lane);
+          if (q < l) {  // uniform: slots l.. are zero
+            const z a1 = zcjmul(pw[q], ur), b1 = zcjmul(pu[q], ur);
+            d24[2 * q] = rs32(a1.x, b1.x);
+            d24[2 * q + 1] = rs32(a1.y, b1.y);
+          } else {
+            d24[2 * q] = 0.0;
+            d24[2 * q + 1] = 0.0;
+          }
         }
-        wave_reduce_scatter24(dv, lane);
-        if ((lane & 3) == 0) {
-          const int b = 24 * ((lane >> 5) & 1) + 12 * ((lane >> 4) & 1) + 6 * ((lane >> 3) & 1) + 3 * ((lane >> 2) & 1);
+        double d12[12], d6[6];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) red2[wv][b + i] = dv[i];
+        for (int i = 0; i < 12; ++i) d12[i] = (i >> 1) < l || 6 + (i >> 1) < l ? rs16(d24[i], d24[12 + i]) : 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+          d6[i] = (i >> 1) < l || 3 + (i >> 1) < l || 6 + (i >> 1) < l || 9 + (i >> 1) < l
+                      ? sum8(rs8(d12[i], d12[6 + i], lane)) : 0.0;
+        if ((lane & 7) == 0) {
+          const int b = 24 * (lane >> 5) + 12 * ((lane >> 4) & 1) + 6 * ((lane >> 3) & 1);
+#pragma unroll
+          for (int i = 0; i < 6; ++i) red2[wv][b + i] = d6[i];
         }
       }
       __syncthreads();
@@ -364,25 +468,24 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
       // dots from LDS where used: W_q^H u = fin[2q..], U_q^H u = fin[24 + 2q..]
 #define DW(q) mk(fin[2 * (q)], fin[2 * (q) + 1])
 #define DU(q) mk(fin[24 + 2 * (q)], fin[24 + 2 * (q) + 1])
-      z uau;
-      {
-        const int cb_lo = (j + 1) >> 4;
-        z e = lane < nblk - cb_lo ? ldz_sc1(bp + hb * 32 + cb_lo + lane) : mk(0, 0);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) e = zadd(e, shfl_z(e, o));
-        uau = e;
-      }
+      // the hand-off's loads first (independent, one latency): this row's and
+      // row j+1's A u, the u^H A u partials of the column blocks
+      const int cbl = (j + 1) >> 4;
+      z p1 = ldz_sc1(pb + hb * n + j + 1);
+      z p = live ? ldz_sc1(pb + hb * n + r) : mk(0, 0);
+      const z eb = lane < nblk - cbl ? ldz_sc1(bp + hb * 32 + cbl + lane) : mk(0, 0);
+      const z uau = mk(wave_allsum(eb.x), wave_allsum(eb.y));
       // one pass over the panel slots (each dot read once from LDS): Re sum
       // conj(dU) dW for K, row j+1's p (every thread the same way), this row's p
       double sd = 0;
-      z p1 = ldz_sc1(pb + hb * n + j + 1);
-      z p = live ? ldz_sc1(pb + hb * n + r) : mk(0, 0);
 #pragma unroll
       for (int q = 0; q < CNB; ++q) {
-        const z dw = DW(q), du = DU(q);
-        sd += du.x * dw.x + du.y * dw.y;  // Re(conj(dU) dW)
-        p1 = zsub(p1, zadd(zmul(Nx[(j + 1) & 1][0][q], dw), zmul(Nx[(j + 1) & 1][1][q], du)));
-        p = zsub(p, zadd(zmul(pu[q], dw), zmul(pw[q], du)));
+        if (q < l) {  // uniform: slots l.. are zero
+          const z dw = DW(q), du = DU(q);
+          sd += du.x * dw.x + du.y * dw.y;  // Re(conj(dU) dW)
+          p1 = zsub(p1, zadd(zmul(Nx[(j + 1) & 1][0][q], dw), zmul(Nx[(j + 1) & 1][1][q], du)));
+          p = zsub(p, zadd(zmul(pu[q], dw), zmul(pw[q], du)));
+        }
       }
       const double K = 0.5 * t * t * (uau.x - 2.0 * sd);
       rw = zsub(zsc(p1, t), zsc(u0, K));
@@ -411,12 +514,25 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
       for (int b0 = 0; b0 < nown; b0 += 4) {
         const int nb = nown - b0 < 4 ? nown - b0 : 4;
         for (int r0 = pe; r0 < n; r0 += 64) {
+          // this wave's outputs of the tile: the stored values first (in flight
+          // while the panel rows are staged and the MFMAs run)
+          z v0[2][4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int c = 16 * (me + G * (k0 + b0 + tc0 + h)) + ml;
+            const bool cok = tc0 + h < nb && c >= pe && c < n;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int rg = r0 + 16 * tr + kl + 4 * rr;
+              v0[h][rr] = (cok && rg < n) ? ldz_g(S + (size_t)rg * n + c) : mk(0, 0);
+            }
+          }
           __syncthreads();
           if (r >= r0 && r < r0 + 64) {
 #pragma unroll
             for (int q = 0; q < CNB; ++q) { Sg[(r - r0) * CNB + q] = pu[q]; Sg[(64 + r - r0) * CNB + q] = pw[q]; }
           }
-          {
+          if (r0 == pe) {  // the batch's columns: staged once
             const int cbr = r >> 4;
             const int kk = (cbr - me) / G - k0 - b0;
             if (cbr >= me && (cbr - me) % G == 0 && kk >= 0 && kk < nb) {
@@ -450,8 +566,7 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
               for (int rr = 0; rr < 4; ++rr) {
                 const int rg = r0 + 16 * tr + kl + 4 * rr;
                 if (rg < n) {
-                  const z v0 = ldz_g(S + (size_t)rg * n + c);
-                  const z v = mk(v0.x - cr[rr], v0.y - ci[rr]);
+                  const z v = mk(v0[h][rr].x - cr[rr], v0[h][rr].y - ci[rr]);
                   stz_g(Ab + (size_t)rg * n + c, v);
                   if (c - pe < CNB) stz_sc1(xc + (size_t)(nxp * CNB + c - pe) * n + rg, v);
                 }

@@ -120,3 +120,62 @@ def test_maxm_boundary_threshold(eng, monkeypatch):
     for r, r0 in zip(res, ref):
         assert r[0] == r0[0]
         assert np.abs(r[2] @ r[3] - r0[2] @ r0[3]).max() <= 1e-12 * np.abs(r0[2] @ r0[3]).max()
+
+
+def _decomp_env(monkeypatch, env, Ms, cutoff, maxm):
+    from optimalcontrolmps_amd.native import Engine
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = Engine(L, p, NPART, 1.0, 0.005, 1e-8, 512, engine="hbm")
+    res = e.denmat_decomp(Ms, cutoff, maxm)
+    st = e.path_stats()
+    e.close()
+    for k in env:
+        monkeypatch.delenv(k)
+    return res, st
+
+
+def test_coop_members_bitwise_and_vs_one_cu(monkeypatch):
+    """k_heev_vals_coop (hbm_coop.hpp): the multi-CU reduction gives the same
+    bits whatever the number G of workgroups per block (1, 3, 8, 16: the
+    host picks G from the CUs a launch leaves, so batched / pipelined runs must
+    not depend on it), matches numpy, and matches the one-CU kernels
+    (OCG_HBM_COOP=0) to rounding; orders 209..512 (config 5's sectors at
+    chi = 512)"""
+    rng = np.random.default_rng(606)
+    shapes = [(209, 230), (256, 300), (384, 384), (512, 640)]
+    Ms = [block(rng, n, c, np.exp(-np.arange(n) / 9.0)) for n, c in shapes]
+    ref, st = _decomp_env(monkeypatch, {"OCG_HBM_COOPG": "1"}, Ms, 1e-8, 512)
+    assert st["coop_groups"] == len(Ms) and st["coop_fallbacks"] == 0
+    for M, r in zip(Ms, ref):
+        check(M, r, 1e-8, 512)
+    for g in ("3", "8", "16"):
+        res, st = _decomp_env(monkeypatch, {"OCG_HBM_COOPG": g}, Ms, 1e-8, 512)
+        assert st["coop_fallbacks"] == 0
+        for r, r0 in zip(res, ref):
+            assert r[0] == r0[0] and np.array_equal(r[1], r0[1]), g
+            assert np.array_equal(r[2], r0[2]) and np.array_equal(r[3], r0[3]), g
+    one, st = _decomp_env(monkeypatch, {"OCG_HBM_COOP": "0"}, Ms, 1e-8, 512)
+    assert st["coop_groups"] == 0
+    for r, r0 in zip(one, ref):
+        assert r[0] == r0[0]
+        assert np.abs(r[2] @ r[3] - r0[2] @ r0[3]).max() <= 1e-11 * np.abs(r0[2] @ r0[3]).max()
+
+
+def test_coop_fallback_one_cu(monkeypatch):
+    """a group that gives up a wait (OCG_HBM_COOP_TMO=0: at its first wait)
+    raises its abort word; k_heev_vals_coop_fix restores the block's lower
+    triangle from the untouched upper one and reduces it on one CU: the
+    result is the one-CU kernel's on that (exactly Hermitian) block, i.e. the
+    one-CU kernel's to rounding (the Gram GEMM's two triangles differ in the
+    last bits), and path_stats counts it"""
+    rng = np.random.default_rng(707)
+    Ms = [block(rng, n, c, np.exp(-np.arange(n) / 7.0)) for n, c in [(240, 260), (400, 420)]]
+    fb, st = _decomp_env(monkeypatch, {"OCG_HBM_COOP_TMO": "0", "OCG_HBM_COOPG": "4"}, Ms, 1e-8, 512)
+    assert st["coop_fallbacks"] == len(Ms)
+    one, _ = _decomp_env(monkeypatch, {"OCG_HBM_COOP": "0", "OCG_HBM_BIGMIN": "193"}, Ms, 1e-8, 512)
+    for M, r, r1 in zip(Ms, fb, one):
+        check(M, r, 1e-8, 512)
+        assert r[0] == r1[0]
+        assert np.abs(r[1][:r[0]] - r1[1][:r[0]]).max() <= 1e-13 * r1[1][0]
+        assert np.abs(r[2] @ r[3] - r1[2] @ r1[3]).max() <= 1e-11 * np.abs(r1[2] @ r1[3]).max()

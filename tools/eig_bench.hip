@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <vector>
 #include "hbm_device.hpp"
+#define COOP_GRID(G, B) (8 * (G) * (((B) + 7) / 8))
 using namespace hbm;
 using cd = std::complex<double>;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -89,7 +90,7 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(e0));
     if (coopG > 0) {
       CK(hipMemsetAsync(dctl, 0, sizeof(int) * kCoopCtl * B, 0));
-      hipLaunchKernelGGL(k_heev_vals_coop, dim3(8 * coopG * ((B + 7) / 8)), dim3(CPT), 0, 0, dP, didx, B, coopG, dctl,
+      hipLaunchKernelGGL(k_heev_vals_coop, dim3(COOP_GRID(coopG, B)), dim3(CPT), 0, 0, dP, didx, B, coopG, dctl,
                          coop_tmo);
       hipLaunchKernelGGL(k_heev_vals_coop_fix, dim3(B), dim3(VBG), 0, 0, dP, didx, dctl, nullptr);
     } else if (n > RNMAX && n <= kBigMax && !getenv("EIG_OLD")) {
