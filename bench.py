@@ -402,8 +402,30 @@ def run_env():
     """the run-time settings a line's numbers depend on, read back from this
     process's environment (GPU_MAX_HW_QUEUES: hardware queues per process, HIP's
     default 4 when unset; the GPU box exports 4)"""
-    keys = ("GPU_MAX_HW_QUEUES", "OMP_NUM_THREADS", "OCG_HBM_PRIO", "OCG_HBM_PIPE", "HIP_VISIBLE_DEVICES")
-    return {k: os.environ.get(k) for k in keys}
+    keys = ("GPU_MAX_HW_QUEUES", "OMP_NUM_THREADS", "OCG_HBM_PRIO", "OCG_HBM_PIPE", "OCG_HBM_COOP",
+            "HIP_VISIBLE_DEVICES")
+    env = {k: os.environ.get(k) for k in keys}
+    env["native_lib"] = native_lib_record()
+    return env
+
+
+def native_lib_record():
+    """which HIP library this process loaded: bench.py never compiles; it loads the
+    in-tree liboptimalcontrolmps_amd.so that __graft_entry__.build() (or
+    native.build_native()) compiled before the tree was shipped.  `stale` is
+    true when a csrc/ source or include/ocmps.h is newer than the library."""
+    import hashlib
+    from optimalcontrolmps_amd import native
+    path = native.LIB_PATH
+    if not os.path.exists(path):
+        return {"path": None}
+    with open(path, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    mt = os.path.getmtime(path)
+    newest = max(os.path.getmtime(x) for x in native.sources())
+    return {"path": os.path.relpath(path, ROOT), "sha16": sha,
+            "mtime_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(mt)),
+            "compiled_by_this_process": False, "stale": bool(newest > mt)}
 
 
 def st_traj_ms_per_step(eng, Nt):
@@ -915,6 +937,7 @@ def cpu_baseline_c5(ini, Nt, threads):
     row_steps = rows * (rows - 1) // 2
     est = t50 * ((Nt - 1) + 3.0 * Nt / th + (row_steps + 3.0 * rows) / th)
     return {"value": rows / est, "unit": "rows/s", "cores": th, "kind": "port", "estimated": True,
+            "measured_fixture_pair": c5_fixture_pair(),
             "measured_step_s_L12_1thread": t12, "model_ratio_L50_over_L12": ratio, "priced_step_s_L50": t50,
             "host_threads_available": avail, "nproc": os.cpu_count(),
             "sample": f"one chi=512 step of the 12-site config-5 chain (tests/golden/c5_w512.npz) on the C++ CPU "
@@ -922,6 +945,41 @@ def cpu_baseline_c5(ini, Nt, threads):
                       f"x{ratio:.1f} to the L=50 state by a flop model of the bond dims; the N_t={Nt} getHessian "
                       f"priced from it at {th} threads (psi || xi serial, dH = 3 steps, xiH and rows over the threads, "
                       f"overlaps not priced, so the estimate favours the CPU)"}
+
+
+def c5_fixture_pair():
+    """A MEASURED chi = 512 getHessian on both sides, the same sample: the 12-site
+    config-5 chain of tests/golden/c5_w512h9.npz (psi_init = the saturated state,
+    psi_target = it stepped three times by the oracle, both at chi = 512, N_t = 9
+    GRAPE controls).  CPU: the oracle's getHessian that made the fixture
+    (make_c5w512_fixture.py hess9: wall seconds and threads stored in the file;
+    timed in the build container, 8 cores, not on this box: 30 min of CPU).  GPU:
+    the same getHessian on this box's MI355X now (HBM engine, pipelined), with
+    max|dH| / max|H| against the oracle's."""
+    from optimalcontrolmps_amd.native import MPS, Engine
+    gd = os.path.join(ROOT, "tests", "golden")
+    f9 = os.path.join(gd, "c5_w512h9.npz")
+    if not os.path.exists(f9):
+        return None
+    c = C5
+    zs = np.load(os.path.join(gd, "c5_w512.npz"), allow_pickle=False)
+    z = np.load(f9, allow_pickle=False)
+    Lx, nt = 12, len(z["u"])
+    ini = MPS(Lx, c["p"], Lx, zs["dims"], zs["data"])
+    tgt = MPS(Lx, c["p"], Lx, z["tdims"], z["tdata"])
+    eng = Engine(Lx, c["p"], Lx, c["J"], c["tstep"], c["cutoff"], c["maxm"], engine="hbm")
+    eng.set_states(tgt, ini)
+    eng.hessian(z["u"])  # warm-up (allocations)
+    t0 = time.perf_counter()
+    H, _, _ = eng.hessian(z["u"])
+    tg = time.perf_counter() - t0
+    eng.close()
+    rows = nt - 2
+    cpu_s = float(z["secs"][0])
+    return {"sample": f"L=12 p=9 chi=512 chain, N_t={nt} getHessian ({rows} rows), tests/golden/c5_w512h9.npz",
+            "cpu_oracle_s": cpu_s, "cpu_threads": int(z["threads"][0]), "cpu_where": "build container (8 cores)",
+            "cpu_rows_per_s": rows / cpu_s, "gpu_s": tg, "gpu_rows_per_s": rows / tg,
+            "max_dH_rel": float(np.abs(H - z["H"]).max() / np.abs(z["H"]).max())}
 
 
 def cpu_threads_available():

@@ -2536,6 +2536,29 @@ int hbm_div_t(hbm_engine* h, double* divT) {
 // instead of 410 GB), the same N-1 dependent steps per chain, and the same
 // states, overlaps and numbers bit for bit (every HBM-engine kernel is
 // batch-independent and deterministic).  Leaves no device trajectories.
+// A call that grows the state heap for slots it does not keep gives them back,
+// down to the heap it began with, on success (done(): a device failure there is
+// the call's status) and on failure (the destructor, errors swallowed while the
+// guard unwinds), so later memory decisions (hipMemGetInfo) see the HBM free.
+struct HeapRestore {
+  hbm::Engine& E;
+  size_t keep;
+  bool ok = false;
+  explicit HeapRestore(hbm::Engine& e) : E(e), keep(e.heap_slots) {}
+  void done() {
+    ok = true;
+    E.shrink_states(keep);
+  }
+  ~HeapRestore() {
+    if (ok) return;
+    try {
+      E.drain();
+      E.shrink_states(keep);
+    } catch (...) {
+    }
+  }
+};
+
 int hbm_gradient_mid(hbm_engine* h, const double* u, int N, double* divT, double* F) {
   return guard(h, [&] {
     if (!h->have_states) throw hbm::Error(4, "ocg_set_states first");
@@ -2543,6 +2566,7 @@ int hbm_gradient_mid(hbm_engine* h, const double* u, int N, double* divT, double
     hbm::Engine& E = *h->E;
     h->have_psi = h->have_xi = h->have_xih = false;  // the trajectory slots are overwritten
     h->N = 0;
+    HeapRestore heap(E);  // the half trajectories are not kept (the footprint stayed at N + 2 slots)
     E.reserve_states(size_t(N) + 2);
     const int tm = (N - 1) / 2;
     auto slot = [](int t) { return 2 + t; };  // psi_t for t <= tm, xi_t above
@@ -2601,6 +2625,7 @@ int hbm_gradient_mid(hbm_engine* h, const double* u, int N, double* divT, double
     F[0] = Fc.real();
     F[1] = Fc.imag();
     for (int t = 0; t < N; ++t) { divT[2 * t] = dv[t].real(); divT[2 * t + 1] = dv[t].imag(); }
+    heap.done();
   });
 }
 
@@ -2845,9 +2870,19 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
     // every checkpoint stored on the way) when N half-trajectory slots fit, so the
     // row passes recompute only the segments their rows need; else the
     // checkpoint-only pass and divT in the first row pass
+    HeapRestore heap(E);  // checkpoints, half trajectories and segments are not kept
     bool mid = false;
     if (const char* e = std::getenv("OCG_HBM_CKPT_MID")) mid = std::atoi(e) != 0;
-    else mid = true;
+    else {
+      // the middle path's N half-trajectory slots only when they leave room for what
+      // follows: the row batches' chains (B + K + 2, priced as hbm_batch prices them)
+      // and their workspace arenas, i.e. the new slots within half the free HBM
+      // (an unbudgeted reservation starved the later chain pools)
+      size_t fr = 0, tot = 0;
+      (void)hipMemGetInfo(&fr, &tot);
+      const double slots = double(R) + std::max(double(N), 3.0 * (K + 1));
+      mid = heap_growth_bytes(h, slots) <= 0.5 * double(fr);
+    }
     if (mid) {
       try {
         E.reserve_states(size_t(R) + std::max<size_t>(size_t(N), size_t(3) * (K + 1)));
@@ -3053,6 +3088,7 @@ int hbm_hessian_ckpt(hbm_engine* h, const double* u, int N, const int* rows, int
     }
     for (int t = 0; t < N; ++t) { divT[2 * t] = dv[t].real(); divT[2 * t + 1] = dv[t].imag(); }
     tall.stop();
+    heap.done();
   });
 }
 
