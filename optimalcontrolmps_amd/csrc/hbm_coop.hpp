@@ -59,6 +59,9 @@ constexpr int CNB = 12;       // panel width
 constexpr int CMB = 8;        // own 16-column blocks per matvec pass
 constexpr int kCoopCtl = 64;  // ints of control words per group: counter at 0, abort word at 32
 constexpr int kCoopMaxG = 16;
+#ifndef COOP_MV_UNROLL
+#define COOP_MV_UNROLL 1  // 8-row load batches of a chunk unrolled (each batch one L2 round trip)
+#endif
 #ifndef COOP_MODEA_MIN
 #define COOP_MODEA_MIN 24  // own 16-column blocks from which each wave sums whole column groups itself
 #endif
@@ -227,21 +230,38 @@ __device__ __forceinline__ double sum8(double v) {
 // conj(A[k][col]) u_k summed over the 32 rows of chunk c in row order (explicit
 // fma: the same bits wherever it is called; rows <= j and invalid columns are
 // zeros).  Loads in batches of 8 (one L2 round trip each).
+// Branch-free: every lane loads a valid (clamped) address and the rows or
+// columns outside the trailing block are selected to zero afterwards (an
+// exec-masked load per element cost ~15 instructions of mask bookkeeping).
+__device__ __forceinline__ z zsel0(bool keep, z v) { return mk(keep ? v.x : 0.0, keep ? v.y : 0.0); }
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+// buffer resource over an n x n complex block: 32-bit offsets, and loads past
+// its end return zeros (rows >= n)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t zblock_rsrc(const z* S, int n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<z*>(S), (short)0, unsigned(n) * unsigned(n) * 16u, 0x00020000);
+}
+__device__ __forceinline__ z ldz_buf(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return mk(__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
+            __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32)));
+}
 __device__ __forceinline__ z chunk_acc(const z* __restrict__ S, int n, int col, bool cok, int j, int c, z u0,
                                        const z* LU) {
   z acc = mk(0, 0);
-#pragma unroll 1
+  const __amdgpu_buffer_rsrc_t rs = zblock_rsrc(S, n);
+  const unsigned cb = 16u * unsigned(col < n ? col : n - 1), rb = 16u * unsigned(n);
+#pragma unroll COOP_MV_UNROLL
   for (int hh = 0; hh < 4; ++hh) {
     z av[8];
+    const unsigned k0 = unsigned(32 * c + 8 * hh);
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) av[s8] = ldz_buf(rs, cb + (k0 + s8) * rb);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) {
       const int k = 32 * c + 8 * hh + s8;
-      av[s8] = (cok && k > j && k < n) ? ldz_g(S + (size_t)k * n + col) : mk(0, 0);
-    }
-#pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) {
-      const int k = 32 * c + 8 * hh + s8;
-      const z uk = k == j + 1 ? u0 : LU[k];
+      av[s8] = zsel0(cok && k > j && k < n, av[s8]);
+      const z lk = LU[k];
+      const z uk = k == j + 1 ? u0 : lk;
       acc.x = fma(av[s8].x, uk.x, fma(av[s8].y, uk.y, acc.x));
       acc.y = fma(av[s8].x, uk.y, fma(-av[s8].y, uk.x, acc.y));
     }
@@ -522,10 +542,11 @@ __global__ __launch_bounds__(CPT, 1) void k_heev_vals_coop(const EProb* __restri
             const int c = 16 * (me + G * (k0 + b0 + tc0 + h)) + ml;
             const bool cok = tc0 + h < nb && c >= pe && c < n;
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
+            for (int rr = 0; rr < 4; ++rr) {  // clamped address, unconditional load (used only where valid)
               const int rg = r0 + 16 * tr + kl + 4 * rr;
-              v0[h][rr] = (cok && rg < n) ? ldz_g(S + (size_t)rg * n + c) : mk(0, 0);
+              v0[h][rr] = ldz_g(S + (size_t)(rg < n ? rg : n - 1) * n + (c < n ? c : n - 1));
             }
+            (void)cok;
           }
           __syncthreads();
           if (r >= r0 && r < r0 + 64) {
