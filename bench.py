@@ -72,6 +72,9 @@ def parse_args(argv=None):
     ap.add_argument("--last-rows", type=int, default=0,
                     help="c4rows / c5rows: only the last R interior rows of H (R >= 1; with --c4-nt 801 / --c5-nt "
                          "1001 the full horizon, where config 5 selects the trajectory checkpointing by itself)")
+    ap.add_argument("--row-stride", type=int, default=1,
+                    help="c4rows / c5rows: every S-th interior row only (rows 1, 1 + S, ...): a sample of a full "
+                         "horizon whose rows span every length; the whole getHessian is priced from it")
     ap.add_argument("--state-cache", default="",
                     help="c4/c5 workloads: npz of psi_init and psi_target, loaded when it exists, else written after "
                          "they are prepared (so a profiled command holds only getHessian launches)")
@@ -206,7 +209,12 @@ def slice_blocks(args):
         common.append("--no-cpu-baseline")
     jobs = [("config4_slice", ["--workload", "c4rows", "--c4-nt", "33", "--steps", "2", "--warmup", "1",
                                "--c4-cpu-nt", str(args.c4_cpu_nt)]),
-            ("config5_slice", ["--workload", "c5rows", "--c5-nt", "17", "--steps", "1", "--warmup", "1"])]
+            ("config5_slice", ["--workload", "c5rows", "--c5-nt", "17", "--steps", "1", "--warmup", "1"]),
+            # config 4 at its stated horizon (N_t = 801, GROUP M = 40): every 25th row (32 rows of every
+            # length, 13,136 of 318,801 row-steps) and the whole precompute, measured; the full
+            # getHessian priced from it (366 s whole, r04/r05: too long for this command)
+            ("config4_horizon_sample", ["--workload", "c4rows", "--c4-nt", "801", "--row-stride", "25", "--steps",
+                                        "1", "--warmup", "0", "--c4-cpu-nt", str(args.c4_cpu_nt)])]
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
     out = {}
@@ -684,9 +692,12 @@ def bench_c4(args):
 
     R = args.last_rows if (args.last_rows and not grad) else Nt - 2
     first = Nt - 1 - R   # the first row of the computed set
+    stride = max(1, args.row_stride)
+    sel = [r for r in range(first, Nt - 1) if (r - 1) % stride == 0]   # the computed rows
+    R = len(sel)
 
     def rows_of(uu, rows):
-        return eng.hessian(uu, [r for r in rows if r >= first])
+        return eng.hessian(uu, [r for r in rows if r >= first and (r - 1) % stride == 0])
 
     def one(s):
         if grad:
@@ -738,7 +749,7 @@ def bench_c4(args):
         eng.propagate(control(nsteps_all), 1)
         t_sc = time.perf_counter() - t_sc
     steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
-    row_steps = R * (R - 1) // 2   # row i steps from i to N_t-2
+    row_steps = sum(Nt - 2 - r for r in sel)   # row i steps from i to N_t-2
     paths = eng.path_stats()
     reps = 1 if strong else world   # independent Hessians / gradients per step
     sweep = args.steps * (steps_traj * (world if (strong or grad) else reps) + (0 if grad else row_steps * reps))
@@ -769,7 +780,9 @@ def bench_c4(args):
                                     f"config {5 if c5 else 4} chain, getHessian"
                                     + (f" GROUP M={M} (convertControl, regularisation gamma={gamma}, "
                                        f"convertHessian on the device)" if M else " GRAPE")
-                                    + (f" over the full horizon N_t={Nt}, the last {R} rows ({row_steps} row-steps)"
+                                    + (f" over the full horizon N_t={Nt}, every {stride}-th row: {R} rows "
+                                       f"({row_steps} of {(Nt - 2) * (Nt - 3) // 2} row-steps)" if stride > 1 else
+                                       f" over the full horizon N_t={Nt}, the last {R} rows ({row_steps} row-steps)"
                                        if R < Nt - 2 else
                                        f" over a T slice N_t={Nt} ({Nt - 2} rows, {row_steps} row-steps)")),
                        "engine": "HBM-resident (hbm.hip)", "parallelism": par},
@@ -792,6 +805,19 @@ def bench_c4(args):
             res["hessian_path"] = {"pipelined": paths["pipe_runs"], "pipeline_fallbacks": paths["pipe_fallbacks"],
                                    "checkpointed": paths["ckpt_runs"],
                                    "checkpoint_segment": paths["ckpt_k"] or None}
+        if stride > 1 and not grad:
+            # the sample's parts (hbm timers: kind 3 = the row batches of the two-phase path). The
+            # rows of a sample run in smaller lockstep batches than the whole Hessian's (32 rows vs
+            # 799 joining over the horizon), so their row-step rate is a lower bound of the whole
+            # run's; the whole getHessian is not priced from it (measured whole: 359-366 s, r04/r05)
+            rows_ms = eng.stats(3)["ms"] / args.steps
+            res["horizon_sample"] = {
+                "rows": R, "of_rows": Nt - 2, "row_steps": row_steps, "of_row_steps": (Nt - 2) * (Nt - 3) // 2,
+                "precompute_ms": 1e3 * elapsed / args.steps - rows_ms, "rows_ms": rows_ms,
+                "row_steps_per_s": row_steps / max(rows_ms * 1e-3, 1e-9),
+                "whole_getHessian_measured_s": [359, 366],
+                "whole_source": "profiles/r04_bench_c4full_prio.json, profiles/r05_bench_c4full_profiled.json "
+                                "(same config-4 code path: the multi-CU eigensolver serves orders >= 209 only)"}
         res["env"] = run_env()
         if world == 1 and not args.no_cpu_baseline and not grad and not args.profiled:
             res["cpu_baseline"] = (cpu_baseline_c5(ini, Nt, args.cpu_threads) if c5 else
