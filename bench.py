@@ -86,7 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--multi", type=int, default=1,
                     help="K control vectors per GPU in one ocg_hessian_multi call (one pipeline launch for all K); "
                          "value = rows of all K per second")
-    ap.add_argument("--profile-tag", default="r05")
+    ap.add_argument("--profile-tag", default="r06")
     ap.add_argument("--profiled", action="store_true",
                     help="run only the warm-up and timed getHessian calls (no single-chain probe, no config-2 "
                          "block, no config-4 / config-5 slice blocks, no CPU baseline): the command rocprofv3 "
