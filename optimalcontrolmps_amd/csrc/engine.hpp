@@ -45,6 +45,9 @@ struct OcgParams {
   const int* fplan;         // plan image of the one-wave padded chain (fast_chain.hpp), or null:
                             // every step of the kernels that step runs on it
   int fast_off;             // byte offset of its region in the dynamic LDS
+  const int* oplan;         // overlap plan of the padded layout (fast_overlap.hpp), or null: the
+                            // row overlaps of getHessian run on the general contraction
+  int ovl_bytes;            // LDS of the padded overlap (k_row_overlaps_pad; <= fast_off)
 };
 #define OCG_ERR_JACOBI 1
 #define OCG_ERR_WATCHDOG 2

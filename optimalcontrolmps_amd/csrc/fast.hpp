@@ -63,5 +63,29 @@ enum {
 
 static_assert(kOhGrp % 4 == 0 && kOhNewBond < 8, "b128 reads of the op header");
 
+// Overlap plan (fast_overlap.hpp; host builder build_overlap_plan in fast_plan.hpp):
+// <X|Y> of two compact-format states contracted in the padded layout,
+// E_k[q'] = sum_n X_(q'-n,n)^H E_(k-1)[q'-n] Y_(q'-n,n), every index fixed by the
+// rank bounds.  Header ints, then the tables at the offsets the header holds:
+constexpr int kOvMaxE = 128;  // environment elements per bond (sum over sectors of D^2)
+constexpr int kOvMaxP = 6;    // local dimension (the unrolled stage-2 sum over n)
+enum {
+  kOvL = 0, kOvQ1, kOvP, kOvNp, kOvNblk,
+  kOvMaxSite,  // largest padded site
+  kOvMaxEn,    // largest environment
+  kOvD,        // bounds D[(L+1) * Q1]
+  kOvEo,       // environment offsets eo[(L+1) * Q1] (prefix over sectors of D^2)
+  kOvEn,       // environment sizes en[L+1]
+  kOvPo,       // padded block offsets within the site po[(L+2) * Q1 * p], -1: none
+  kOvSb,       // site starts sb[L+2] in the padded image
+  kOvElo,      // environment element lists: bond b's at elo[b] (L+2 ints)
+  kOvEl,       // element x of E_b: q | c' << 8 | c << 12 | D(b, q) << 16
+  kOvLs,       // per padded element, int4 (16-byte aligned):
+               //   rows dims idx | cols dims idx << 16, block | first block << 16,
+               //   a | c << 4 | D(k-1, q) << 8 | D(k, q+n) << 12 | eo(k-1, q) << 16, site_base[k]
+  kOvBlk,      // per block: rows dims idx | cols dims idx << 16 (the compact size)
+  kOvNint,     // ints of the plan
+  kOvHdr = 20
+};
 }  // namespace fastp
 }  // namespace ocg

@@ -435,4 +435,101 @@ inline int fast_lds_bytes(const std::vector<int>& plan, const OcgParams& P) {
   return plan[kHZTot] * 16 + kFastDbl * 8 + (fast_int_words(P, plan[kHNblk]) + int(plan.size())) * 4;
 }
 
+// The overlap plan of the padded layout (fast.hpp kOv*): the bounds, the
+// environment layout per bond, the padded block offsets, per environment
+// element its indices, per padded element its compact-format source and its
+// stage-1 indices.  Empty (the general overlap runs) when a bound, an
+// environment or a site is beyond the packed fields.
+inline std::vector<int> build_overlap_plan(const OcgParams& P, const std::vector<int>& md) {
+  using namespace ocg::fastp;
+  const int L = P.L, p = P.p, Q = P.Q, Q1 = P.Q1;
+  auto D = [&](int b, int q) { return (b < 0 || b > L || q < 0 || q > Q) ? 0 : md[size_t(b) * Q1 + q]; };
+  if (p > kOvMaxP) return {};
+  std::vector<int> eo(size_t(L + 1) * Q1, 0), en(L + 1, 0);
+  int maxen = 1;
+  for (int b = 0; b <= L; ++b) {
+    int o = 0;
+    for (int q = 0; q <= Q; ++q) {
+      if (D(b, q) > kMaxDm) return {};  // the unrolled sums
+      eo[size_t(b) * Q1 + q] = o;
+      o += D(b, q) * D(b, q);
+    }
+    en[b] = o;
+    maxen = std::max(maxen, o);
+    if (o > kOvMaxE) return {};
+  }
+  // both ends are one 1 x 1 sector: E_0 = 1 and <X|Y> = E_L
+  if (en[0] != 1 || en[L] != 1) return {};
+  std::vector<int> po(size_t(L + 2) * Q1 * p, -1), sb(L + 2, 0), ls, blk;
+  int np = 0, maxsite = 1;
+  for (int k = 1; k <= L; ++k) {
+    sb[k] = np;
+    const int b0 = int(blk.size());
+    for (int q = 0; q <= Q; ++q)
+      for (int n = 0; n < p && q + n <= Q; ++n) {
+        const int dl = D(k - 1, q), dr = D(k, q + n);
+        if (dl == 0 || dr == 0) continue;
+        const int b = int(blk.size()), ri = (k - 1) * Q1 + q, ci = k * Q1 + q + n;
+        blk.push_back(ri | (ci << 16));
+        po[(size_t(k) * Q1 + q) * p + n] = np - sb[k];
+        for (int a = 0; a < dl; ++a)
+          for (int c = 0; c < dr; ++c) {
+            ls.push_back(ri | (ci << 16));
+            ls.push_back(b | (b0 << 16));
+            ls.push_back(a | (c << 4) | (dl << 8) | (dr << 12) | (eo[size_t(k - 1) * Q1 + q] << 16));
+            ls.push_back(P.site_base[k]);
+          }
+        np += dl * dr;
+      }
+    maxsite = std::max(maxsite, np - sb[k]);
+  }
+  sb[L + 1] = np;
+  if (np == 0 || np > 4096 || int(blk.size()) > 32767 || (L + 1) * Q1 > 32767) return {};
+  std::vector<int> elo(L + 2, 0), el;
+  for (int b = 0; b <= L; ++b) {
+    elo[b] = int(el.size());
+    for (int q = 0; q <= Q; ++q)
+      for (int c = 0; c < D(b, q); ++c)
+        for (int d = 0; d < D(b, q); ++d) el.push_back(q | (c << 8) | (d << 12) | (D(b, q) << 16));
+  }
+  elo[L + 1] = int(el.size());
+  std::vector<int> Dv(size_t(L + 1) * Q1);
+  for (int b = 0; b <= L; ++b)
+    for (int q = 0; q <= Q; ++q) Dv[size_t(b) * Q1 + q] = D(b, q);
+  std::vector<int> I(kOvHdr, 0);
+  auto sec = [&](int slot, const std::vector<int>& v) {
+    while (I.size() & 3) I.push_back(0);  // 16-byte aligned tables
+    I[slot] = int(I.size());
+    I.insert(I.end(), v.begin(), v.end());
+  };
+  I[kOvL] = L;
+  I[kOvQ1] = Q1;
+  I[kOvP] = p;
+  I[kOvNp] = np;
+  I[kOvNblk] = int(blk.size());
+  I[kOvMaxSite] = maxsite;
+  I[kOvMaxEn] = maxen;
+  sec(kOvD, Dv);
+  sec(kOvEo, eo);
+  sec(kOvEn, en);
+  sec(kOvPo, po);
+  sec(kOvSb, sb);
+  sec(kOvElo, elo);
+  sec(kOvEl, el);
+  sec(kOvLs, ls);
+  sec(kOvBlk, blk);
+  while (I.size() & 3) I.push_back(0);
+  I[kOvNint] = int(I.size());
+  return I;
+}
+// LDS of the one-wave overlap (fast_overlap.hpp): plan, two dims / block-offset
+// arrays, the two padded states and their zero slot, T, two environments
+inline int overlap_lds_bytes(const std::vector<int>& I, const OcgParams& P) {
+  using namespace ocg::fastp;
+  auto al = [](int x) { return (x + 3) & ~3; };
+  const int ints = I[kOvNint] + 2 * al(P.nsq) + 2 * al(I[kOvNblk] + 1);
+  const int zs = 2 * (I[kOvNp] + 2) + (I[kOvMaxSite] + 2) + 2 * (I[kOvMaxEn] + 2);
+  return ints * 4 + zs * 16;
+}
+
 }  // namespace ocg_host

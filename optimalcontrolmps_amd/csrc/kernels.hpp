@@ -5,6 +5,7 @@
 
 #include "engine_device.hpp"
 #include "fast_chain.hpp"
+#include "fast_overlap.hpp"
 
 namespace ocg {
 
@@ -171,7 +172,16 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
   double bytes = 0, flops = 0;
   const bool fo = fast_on(P);
   FastChain f(P, smem + P.fast_off, P.fplan, c.PROF);
+  // the padded overlap (fast_overlap.hpp) in the general chain's region, which
+  // the one-wave chain leaves unused: the arithmetic of k_row_overlaps_pad, so
+  // fused == unfused stays bitwise
+  const bool po = fo && P.oplan != nullptr;
+  FastOverlap o(P, smem, po ? P.oplan : nullptr);
   if (fo) {
+    if (po) {
+      __syncthreads();  // load_tables' writes into the region first
+      o.init(P.oplan);
+    }
     f.init(P.fplan, gf, gb);
     f.load(SLOT_D(pool, P, psih_base + i), SLOT_X(pool, P, psih_base + i));
   }
@@ -179,18 +189,28 @@ __device__ OCG_INLINE void body_hessian_rows(char* smem, OcgParams P, const zc* 
   for (int j = i; j + 1 < N; ++j) {
     if (j > i) {
       if (fo) {
-        // the one-wave chain steps; its state goes through the general chain's
-        // LDS copy (compact layout, offsets rebuilt by load) for the overlap
         f.step(u[j - 1], u[j], 1, false);
-        f.store(flat(c.DIMS), flat(c.A));
-        __syncthreads();
-        c.load(flat(c.DIMS), flat(c.A));
+        if (!po) {
+          // the general overlap: the state goes through the general chain's LDS
+          // copy (compact layout, offsets rebuilt by load)
+          f.store(flat(c.DIMS), flat(c.A));
+          __syncthreads();
+          c.load(flat(c.DIMS), flat(c.A));
+        }
       } else {
         c.step(u[j - 1], u[j], 1, false);  // row: no closing gauge move (Chain::step)
       }
     }
-    zc ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
-    const double used = c.mps_used();
+    zc ov;
+    double used;
+    if (po) {
+      o.load(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), nullptr, nullptr);
+      ov = o.contract(f.MP);
+      used = o.compact_size(f.DIM);
+    } else {
+      ov = c.overlap(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), 0);
+      used = c.mps_used();
+    }
     if (threadIdx.x == 0) {
       zc di = divT[i], dj = divT[j];
       double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? normiH : 1.0);  // Re(F <xiH_j|psiH> n_i)
@@ -437,6 +457,59 @@ __device__ OCG_INLINE void body_row_overlaps(char* smem, OcgParams P, const zc* 
     c.sync();  // LDS reuse by the next pair
   }
   flush_stats(c, stats, b, 8.0 * b / 16.0 * 4.0, 0.0);
+}
+
+// body_row_overlaps on the padded layout (fast_overlap.hpp, P.oplan set): one
+// wave per workgroup, the same pairs, the same H_ij assembly
+__device__ inline OCG_INLINE void body_row_overlaps_pad(char* smem, OcgParams P, Pool pool, int xih_base0,
+                                                        const int* rows, int nrows, const int* rbase, Pool rs,
+                                                        const double* rnorm0, const zc* divT0, const zc* Fp, int N,
+                                                        double* H0, double* stats, int K, int cs) {
+  FastOverlap o(P, smem, P.oplan);
+  // the row table after the overlap's region: the (row, column) search of every
+  // pair runs on LDS instead of ~log2(rows) dependent global loads
+  LDS int* RB = (LDS int*)(smem + P.ovl_bytes);
+  LDS int* RW = RB + nrows + 1;
+  o.init(P.oplan);
+  for (int x = threadIdx.x; x <= nrows; x += 64) {
+    RB[x] = rbase[x];
+    if (x < nrows) RW[x] = rows[x];
+  }
+  o.wsync();
+  const int total = RB[nrows];
+  double b = 0;
+  for (int g = blockIdx.x; g < K * total; g += gridDim.x) {
+    const int kc = g / total, gl = g - kc * total;
+    int lo = 0, hi = nrows - 1;  // row r with rbase[r] <= gl < rbase[r+1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (RB[mid] <= gl) lo = mid;
+      else hi = mid - 1;
+    }
+    const int r = lo, i = RW[r], j = i + (gl - RB[r]);
+    const int xih_base = xih_base0 + kc * cs;
+    // the assembly's operands first: their loads overlap the contraction
+    const zc* divT = divT0 + (size_t)kc * N;
+    const zc F = Fp[kc], di = divT[i], dj = divT[j];
+    const double rn = rnorm0[(size_t)kc * nrows + r];
+    const int ny = o.load(SLOT_D(pool, P, xih_base + j), SLOT_X(pool, P, xih_base + j), SLOT_D(rs, P, g),
+                          SLOT_X(rs, P, g));
+    const zc ov = o.contract(o.YP);
+    b += 32.0 * ny;
+    if (threadIdx.x == 0) {
+      double* H = H0 + (size_t)kc * N * N;
+      const double v1 = (F.x * ov.x - F.y * ov.y) * (j > i ? rn : 1.0);  // Re(F <xiH_j|psiH> normiH)
+      const double v2 = -(di.x * dj.x + di.y * dj.y);                  // -Re(divT_i conj(divT_j))
+      const double res = P.dt * P.dt * (v1 + v2);
+      H[(size_t)i * N + j] = res;
+      if (j > i) H[(size_t)j * N + i] = res;
+    }
+    o.wsync();  // LDS reuse by the next pair
+  }
+  if (threadIdx.x == 0 && stats) {
+    atomicAdd(stats + 0, b);
+    atomicAdd(stats + 1, 8.0 * b / 16.0 * 4.0);
+  }
 }
 
 // nsteps steps per state; u holds nsteps+1 controls per state (u_stride apart)

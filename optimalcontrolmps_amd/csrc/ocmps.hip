@@ -103,6 +103,15 @@ __global__ __launch_bounds__(64) void k_row_overlaps_w(OcgParams P, const zc* gf
                              stats, K, cs);
 }
 
+// the row overlaps on the padded layout (fast_overlap.hpp): one wave, ~12 KB
+__global__ __launch_bounds__(64) void k_row_overlaps_pad(OcgParams P, Pool pool, int xih_base, const int* rows,
+                                                         int nrows, const int* rbase, Pool rs, const double* rnorm,
+                                                         const zc* divT, const zc* F, int N, double* H,
+                                                         double* stats, int K, int cs) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_row_overlaps_pad(smem, P, pool, xih_base, rows, nrows, rbase, rs, rnorm, divT, F, N, H, stats, K, cs);
+}
+
 __global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                               Pool pool, const int* slots, int n, const double* u, int u_stride,
                                               int nsteps, int forward, double* stats) {
@@ -258,6 +267,7 @@ struct ocg_ctx {
   double* d_prn = nullptr;    // psiH norms by row slot
   int prn_cap = 0;
   int* d_fplan = nullptr;     // plan image of the one-wave padded chain (null: off)
+  int* d_oplan = nullptr;     // overlap plan of the padded layout (null: off)
   std::string fast_why;       // why it is off
   // trajectory state
   int N = 0;
@@ -532,6 +542,8 @@ static int finish_params(ocg_ctx* c) {
   // the ground state) need no plans
   c->P.fplan = nullptr;
   c->P.fast_off = 0;
+  c->P.oplan = nullptr;
+  c->P.ovl_bytes = 0;
   const char* nf = std::getenv("OCG_NO_FAST");
   if (nf && nf[0] && nf[0] != '0') {
     c->fast_why = "OCG_NO_FAST";
@@ -559,6 +571,26 @@ static int finish_params(ocg_ctx* c) {
   c->P.lds_bytes = off + fbytes;
   c->plan_pe2 = 0;
   c->lds2 = 0;
+  // the padded overlap (fast_overlap.hpp) for getHessian's row overlaps; in
+  // k_hessian_rows it lives in the general chain's region, so it must fit there
+  // (OCG_NO_FAST_OVL=1: the general contraction, A/B and tests)
+#ifndef OCG_PROFILE  // (the diagnostic build's phase counters live in that region)
+  {
+    const char* no = std::getenv("OCG_NO_FAST_OVL");
+    const std::vector<int> ov = ocg_host::build_overlap_plan(c->P, c->md);
+    const int ob = ov.empty() ? 0 : ocg_host::overlap_lds_bytes(ov, c->P);
+    if (!ov.empty() && ob <= off && !(no && no[0] && no[0] != '0')) {
+      HIPCHK(c, hipMalloc(&c->d_oplan, sizeof(int) * ov.size()));
+      HIPCHK(c, hipMemcpyAsync(c->d_oplan, ov.data(), sizeof(int) * ov.size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->P.oplan = c->d_oplan;
+      c->P.ovl_bytes = ob;
+      if (std::getenv("OCG_FAST_DUMP"))
+        std::fprintf(stderr, "[fast ovl] np %d nblk %d ints %d bytes %d\n", ov[ocg::fastp::kOvNp],
+                     ov[ocg::fastp::kOvNblk], ov[ocg::fastp::kOvNint], ob);
+    }
+  }
+#endif
 #ifdef OCG_PROFILE
   c->lds_alias = 0;  // the diagnostic build's phase counters live in the general chain's LDS
 #else
@@ -750,6 +782,7 @@ int ocg_destroy(ocg_ctx* c) {
   if (c->d_rnorm) (void)hipFree(c->d_rnorm);
   if (c->d_idx2) (void)hipFree(c->d_idx2);
   if (c->d_fplan) (void)hipFree(c->d_fplan);
+  if (c->d_oplan) (void)hipFree(c->d_oplan);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   for (auto& e : c->evh)
     if (e) (void)hipEventDestroy(e);
@@ -1603,7 +1636,21 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   }
   const size_t ktotal = size_t(K) * total;
   const int rgrid = (rov_grid > 0 && size_t(rov_grid) < ktotal) ? rov_grid : int(ktotal);
-  if (total > 0 && rov_w)
+  if (total > 0 && c->P.oplan) {
+    // the padded overlap: one wave and ~12 KB per workgroup, so up to 16 per CU
+    int ncu = 0, lds_cu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, c->device);
+    const int pb = c->P.ovl_bytes + 4 * (2 * nrows + 1);  // + the row table (kernels.hpp)
+    const int per = lds_cu > 0 ? std::max(1, lds_cu / pb) : 8;
+    const size_t pg = rov_env > 0 ? size_t(rov_env) : size_t(std::max(1, ncu)) * std::min(per, 16);
+    const int pgrid = int(std::min(pg, ktotal));
+    if (pb > 65536) HIPCHK(c, hipFuncSetAttribute((const void*)k_row_overlaps_pad,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, pb));
+    hipLaunchKernelGGL(k_row_overlaps_pad, dim3(unsigned(pgrid)), dim3(64), pb, c->stream, c->P,
+                       c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc, c->d_pc + K * N, N,
+                       c->d_H, c->d_stats + 6 * 3, K, cs);
+  } else if (total > 0 && rov_w)
     hipLaunchKernelGGL(k_row_overlaps_w, dim3(unsigned(rgrid)), dim3(64), Po.lds_bytes, c->stream, Po, c->d_gf,
                        c->d_gb, c->d_md, c->pool, c->xih_base(), d_rows, nrows, d_rbase, c->rs, c->d_prn, c->d_pc,
                        c->d_pc + K * N, N, c->d_H, c->d_stats + 6 * 3, K, cs);

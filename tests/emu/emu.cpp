@@ -29,6 +29,7 @@ struct Emu {
   OcgParams P;
   std::vector<int> md;
   std::vector<int> fplan;  // one-wave padded chain plan (empty: off)
+  std::vector<int> oplan;  // padded overlap plan (empty: off)
   std::vector<double> gf, gb;
   int lds = 0;
   std::vector<int> dims;       // pool
@@ -131,6 +132,13 @@ void* emu_new_ex(int L, int p, int Q, double J, double dt, double cutoff, int ma
   e->P.fast_off = off;
   e->lds = off + ocg_host::fast_lds_bytes(e->fplan, e->P);
   e->P.lds_bytes = e->lds;
+  // the padded overlap, as ocmps.hip's finish_params (OCG_NO_FAST_OVL=1: off)
+  const char* no = std::getenv("OCG_NO_FAST_OVL");
+  e->oplan = ocg_host::build_overlap_plan(e->P, e->md);
+  if (!e->oplan.empty() && ocg_host::overlap_lds_bytes(e->oplan, e->P) <= off && !(no && no[0] && no[0] != '0')) {
+    e->P.oplan = e->oplan.data();
+    e->P.ovl_bytes = ocg_host::overlap_lds_bytes(e->oplan, e->P);
+  }
   return e;
 }
 void emu_free(void* h) { delete static_cast<Emu*>(h); }
@@ -277,9 +285,14 @@ void emu_hessian_fused(void* h, const int* dt_, const double* tgt, const int* di
     ocg::body_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), &a, &b, 1, 0, pc.data() + N, e.stats + 3);
   });
   std::memset(H, 0, sizeof(double) * N * N);
+  if (P.oplan) e.lds = std::max(e.lds, P.ovl_bytes + 4 * (2 * nrows + 1));  // + the row table
   launch(e, total, [&](char* smem) {
-    ocg::body_row_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), xih, rows.data(), nrows, rb.data(), rs,
-                               rn.data(), pc.data(), pc.data() + N, N, H, e.stats + 9, 1, 0);
+    if (P.oplan)
+      ocg::body_row_overlaps_pad(smem, P, e.pool(), xih, rows.data(), nrows, rb.data(), rs, rn.data(), pc.data(),
+                                 pc.data() + N, N, H, e.stats + 9, 1, 0);
+    else
+      ocg::body_row_overlaps<NT>(smem, P, e.GF(), e.GB(), e.md.data(), e.pool(), xih, rows.data(), nrows, rb.data(),
+                                 rs, rn.data(), pc.data(), pc.data() + N, N, H, e.stats + 9, 1, 0);
   });
   for (int i = 0; i < N; ++i) { divT[2 * i] = pc[i].x; divT[2 * i + 1] = pc[i].y; }
   F[0] = pc[N].x;

@@ -23,6 +23,7 @@ def lib():
         L.emu_steps.argtypes = [C.c_void_p, ip, dp, dp, C.c_int, C.c_int, ip, dp]
         if hasattr(L, "emu_hessian_fused"):  # absent from the steps-only sanitizer build
             L.emu_hessian_fused.argtypes = [C.c_void_p, ip, dp, ip, dp, dp, C.c_int, dp, dp, dp]
+            L.emu_hessian.argtypes = [C.c_void_p, ip, dp, ip, dp, dp, C.c_int, dp, dp, dp, dp, C.c_int]
         _lib = L
     return _lib
 
@@ -60,4 +61,19 @@ class Emu:
         lib().emu_hessian_fused(self.h, a[0].ctypes.data_as(ip), b[0].ctypes.data_as(dp), a[1].ctypes.data_as(ip),
                                 b[1].ctypes.data_as(dp), uu.ctypes.data_as(dp), N, H.ctypes.data_as(dp),
                                 dv.ctypes.data_as(dp), F.ctypes.data_as(dp))
+        return H.reshape(N, N), dv.view(np.complex128), complex(F[0], F[1])
+
+    def hessian(self, tdims, tdata, idims, idata, u):
+        """the unfused path (trajectories, divT / F, exactApplyMPO batches, k_hessian_rows)"""
+        N = len(u)
+        H = np.zeros(N * N)
+        dv = np.zeros(2 * N)
+        F = np.zeros(2)
+        fid = np.zeros(N)
+        a = [np.ascontiguousarray(v, np.int32) for v in (tdims, idims)]
+        b = [np.ascontiguousarray(v, np.complex128).view(np.float64) for v in (tdata, idata)]
+        uu = np.ascontiguousarray(u, np.float64)
+        lib().emu_hessian(self.h, a[0].ctypes.data_as(ip), b[0].ctypes.data_as(dp), a[1].ctypes.data_as(ip),
+                          b[1].ctypes.data_as(dp), uu.ctypes.data_as(dp), N, H.ctypes.data_as(dp),
+                          dv.ctypes.data_as(dp), F.ctypes.data_as(dp), fid.ctypes.data_as(dp), N)
         return H.reshape(N, N), dv.view(np.complex128), complex(F[0], F[1])

@@ -61,3 +61,28 @@ def test_emulated_fast_pipeline(E):
     assert np.abs(Hf - Ho).max() <= 1e-12 * np.abs(Ho).max()
     assert np.abs(Hf - Hg).max() <= 1e-12 * np.abs(Ho).max()
     assert np.abs(dvf - dvg).max() <= 1e-14 and abs(Ff - Fg) <= 1e-14
+
+
+def test_emulated_padded_overlap(E, monkeypatch):
+    """the row overlaps on the padded layout (csrc/fast_overlap.hpp): fused
+    (k_row_overlaps_pad) == unfused (k_hessian_rows on the one-wave chain)
+    bitwise, both against the general contraction (OCG_NO_FAST_OVL=1) and the
+    oracle"""
+    Lx, px, Qx, J, dt, cut, maxm = 5, 5, 5, 1.0, 0.01, 1e-8, 80
+    di, xi = _gs(Lx, px, Qx, J, 2.5)
+    dtg, xtg = _gs(Lx, px, Qx, J, 50.0)
+    N = 6
+    u = np.random.default_rng(5).uniform(2.0, 10.0, N)
+    e = E.Emu(Lx, px, Qx, J, dt, cut, maxm, True)
+    Hf, dvf, Ff = e.hessian_fused(dtg, xtg, di, xi, u)
+    Hu, dvu, Fu = e.hessian(dtg, xtg, di, xi, u)
+    monkeypatch.setenv("OCG_NO_FAST_OVL", "1")
+    Hg, _, _ = E.Emu(Lx, px, Qx, J, dt, cut, maxm, True).hessian_fused(dtg, xtg, di, xi, u)
+    monkeypatch.delenv("OCG_NO_FAST_OVL")
+    oc = O.OC(O.Stepper(Lx, px, Qx, J, dt, cut, maxm), O.MPS(Lx, px, Qx, dtg, xtg), O.MPS(Lx, px, Qx, di, xi), N, 0.0)
+    Ho = oc.hessian(u, 2)
+    m = np.abs(Ho).max()
+    assert np.array_equal(Hf, Hu)
+    assert np.abs(Hf - Hg).max() <= 1e-13 * m
+    assert np.abs(Hf - Ho).max() <= 1e-12 * m
+    assert not np.array_equal(Hf, Hg)  # the padded contraction ran (a different summation order)
