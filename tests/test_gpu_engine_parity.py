@@ -315,6 +315,30 @@ def test_fused_equals_unfused_config1_full_horizon(states):
     assert np.array_equal(H1, H2)
 
 
+def test_padded_row_overlaps_vs_general(states):
+    """getHessian's row overlaps on the padded layout (csrc/fast_overlap.hpp,
+    k_row_overlaps_pad and k_hessian_rows) against the general contraction
+    (OCG_NO_FAST_OVL=1): the same Hessian to rounding, a different summation
+    order (so the padded kernel really ran), and fused == unfused bitwise on
+    both"""
+    L, p, N, J = 5, 5, 5, 1.0
+    u = np.random.default_rng(29).uniform(2, 10, 41)
+    tgt, ini = st_of(states, L, p, N, J, 50.0), st_of(states, L, p, N, J, 2.5)
+
+    def run():
+        eng = engine(L, p, N, J, 0.01, 1e-8, 80)
+        eng.set_states(tgt, ini)
+        H1, d1, F1 = eng.hessian(u)
+        divT, F, fid, H2 = run_engine_hessian(eng, u, tgt, ini)
+        assert np.array_equal(H1, H2) and np.array_equal(d1, divT) and F1 == F
+        return H1
+
+    Hp = run()
+    Hg = _with_env("OCG_NO_FAST_OVL", "1", run)
+    assert np.abs(Hp - Hg).max() <= 1e-12 * np.abs(Hg).max()
+    assert not np.array_equal(Hp, Hg)
+
+
 def test_long_horizon_rows_exceed_cus(states):
     """N_t = 801 (T = 8 at config 1's dt): 799 Hessian rows, more workgroups
     than the device has CUs.  Roles are taken by ticket, so the pipeline makes
