@@ -84,7 +84,7 @@ def test_main_spawns_without_launcher(monkeypatch):
 
 
 def test_slice_blocks_children(monkeypatch):
-    """the config-4 / config-5 blocks run as fresh `bench.py --workload ...`
+    """the config-4 / config-5 / config-4 horizon blocks run as fresh `bench.py --workload ...`
     interpreters without the rank environment; a failing child leaves an
     `error` field and the other block intact"""
     import subprocess
@@ -100,5 +100,7 @@ def test_slice_blocks_children(monkeypatch):
     out = bench.slice_blocks(bench.parse_args(["--gpus", "1"]))
     assert out["config4_slice"]["value"] == 1.0 and "error" not in out["config4_slice"]
     assert "error" in out["config5_slice"] and "child_wall_s" in out["config5_slice"]
-    assert [c[0][3:5] for c in seen] == [["--workload", "c4rows"], ["--workload", "c5rows"]]
+    assert out["config4_horizon_sample"]["value"] == 1.0
+    assert [c[0][3:5] for c in seen] == [["--workload", "c4rows"], ["--workload", "c5rows"], ["--workload", "c4rows"]]
+    assert "--row-stride" in seen[2][0] and "801" in seen[2][0]
     assert all("RANK" not in env for _, env in seen)

@@ -10,6 +10,7 @@ import os
 import numpy as np
 import pytest
 
+import oracle_ffi as O
 from conftest import state_key
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -54,6 +55,13 @@ def test_ckpt_config1_states_bitwise(states, K, mid):
     H2, d2, F2 = ckpt(eng, u, rows, K, mid)
     assert F1 == F2 and np.array_equal(d1, d2)
     assert np.array_equal(H1, H2)
+    # and the CPU oracle's getHessian of the same inputs (north_star 1e-6)
+    oc = O.OC(O.Stepper(L, p, N, J, 0.01, 1e-8, 80), O.MPS(L, p, N, st(50.0).dims, st(50.0).data),
+              O.MPS(L, p, N, st(2.5).dims, st(2.5).data), len(u), 0.0)
+    Ho = oc.hessian(u, 8)
+    do, Fo = oc.divT_F()
+    assert abs(F2 - Fo) <= 1e-9 and np.abs(d2 - do).max() <= 1e-8 * np.abs(do).max()
+    assert np.abs(H2 - Ho).max() <= 1e-6 * np.abs(Ho).max()
     # a row subset in two batches of the time-major sweep
     sub = [3, 4, 11, 17]
     H3, _, _ = ckpt(eng, u, sub, K, mid)
@@ -106,6 +114,11 @@ def test_gradient_meet_in_the_middle_bitwise(states, N):
     d2, F2 = _mid(eng, u, "1")
     assert F1 == F2 and np.array_equal(d1, d2)
     eng.close()
+    oc = O.OC(O.Stepper(L, p, Q, J, 0.01, 1e-8, 80), O.MPS(L, p, Q, st(50.0).dims, st(50.0).data),
+              O.MPS(L, p, Q, st(2.5).dims, st(2.5).data), N, 0.0)
+    oc.gradient(u)
+    do, Fo = oc.divT_F()
+    assert abs(F2 - Fo) <= 1e-9 and np.abs(d2 - do).max() <= 1e-8 * np.abs(do).max()
 
 
 def test_gradient_meet_in_the_middle_config4_vs_oracle():

@@ -94,6 +94,18 @@ def run_engine_hessian(eng, u, tgt, ini):
     return divT, F, fid, H
 
 
+def oracle_check(H, divT, F, L, p, N, J, dt, cut, maxm, tgt, ini, u, threads=8):
+    """the CPU oracle's getHessian of the same inputs, so that a path-equality
+    test also pins parity: H to the north_star 1e-6 of its scale, divT / F to
+    1e-8 / 1e-9 (test_hessian_multi_vs_oracle's bounds)"""
+    oc = O.OC(O.Stepper(L, p, N, J, dt, cut, maxm if maxm > 0 else 5000), as_orc(tgt), as_orc(ini), len(u), 0.0)
+    Ho = oc.hessian(u, threads)
+    do, Fo = oc.divT_F()
+    assert abs(F - Fo) <= 1e-9
+    assert np.abs(divT - do).max() <= 1e-8 * np.abs(do).max()
+    assert np.abs(H - Ho).max() <= 1e-6 * np.abs(Ho).max()
+
+
 @pytest.mark.parametrize("case", GOLDEN, ids=[c[0] for c in GOLDEN])
 def test_trajectories_gradient_hessian_vs_golden(states, oracle_golden, case):
     name, (L, p, N, J), Ui, Uf, dt, cut, maxm = case
@@ -203,6 +215,8 @@ def test_fused_equals_unfused_bitwise(states):
     rows = list(range(1, len(u) - 1))
     parts = [eng.hessian(u, rows[k::4])[0] for k in range(4)]
     assert np.array_equal(sum(parts), H2)
+    oracle_check(H2, divT2, F2, L, p, N, J, 0.01, 1e-8, 80, st_of(states, L, p, N, J, 50.0),
+                 st_of(states, L, p, N, J, 2.5), u)
 
 
 def _with_plans(flag, fn):
@@ -243,6 +257,7 @@ def test_plans_bitwise_neutral(states, L, p, N, J, Ui, Uf, cut):
     H0, d0, F0, lds0 = _with_plans(False, run)
     assert lds1 > lds0  # the plan slots are really there
     assert np.array_equal(H1, H0) and np.array_equal(d1, d0) and F1 == F0
+    oracle_check(H1, d1, F1, L, p, N, J, 0.01, cut, 80, tgt, ini, u)
 
 
 def test_truncation_heavy_vs_oracle(states):
@@ -313,6 +328,7 @@ def test_fused_equals_unfused_config1_full_horizon(states):
     divT, F, fid, H2 = run_engine_hessian(eng, u, tgt, ini)
     assert np.array_equal(d1, divT) and F1 == F
     assert np.array_equal(H1, H2)
+    oracle_check(H1, d1, F1, L, p, N, J, 0.01, 1e-8, 80, tgt, ini, u)
 
 
 def test_padded_row_overlaps_vs_general(states):
@@ -337,6 +353,9 @@ def test_padded_row_overlaps_vs_general(states):
     Hg = _with_env("OCG_NO_FAST_OVL", "1", run)
     assert np.abs(Hp - Hg).max() <= 1e-12 * np.abs(Hg).max()
     assert not np.array_equal(Hp, Hg)
+    oc = O.OC(O.Stepper(L, p, N, J, 0.01, 1e-8, 80), as_orc(tgt), as_orc(ini), len(u), 0.0)
+    Ho = oc.hessian(u, 8)
+    assert np.abs(Hp - Ho).max() <= 1e-6 * np.abs(Ho).max()
 
 
 def test_long_horizon_rows_exceed_cus(states):
@@ -411,6 +430,7 @@ def test_hessian_multi_shared_cu_layout_bitwise(states, monkeypatch):
     for k in range(2):
         Hs, ds, Fs = eng.hessian(U[k])
         assert np.array_equal(Hm[k], Hs) and np.array_equal(dm[k], ds) and Fm[k] == Fs, k
+        oracle_check(Hs, ds, Fs, L, p, N, J, 0.01, 1e-8, 80, tgt, ini, U[k])
 
 
 @pytest.mark.parametrize("K", [1, 5])
