@@ -253,6 +253,18 @@ struct Engine {
   int thresh_min = (std::getenv("OCG_HBM_THRESH") && std::atoi(std::getenv("OCG_HBM_THRESH")) > 1)
                        ? std::atoi(std::getenv("OCG_HBM_THRESH"))
                        : 48;
+  // register-path Gram blocks of order >= split_min leave their multisection to
+  // k_heev_bisect_split (SPE eigenvalues per workgroup on many CUs) and
+  // k_heev_bisect_fill; OCG_HBM_SPLITMIN=n moves the threshold, 0 turns it off
+  int split_min = std::getenv("OCG_HBM_SPLITMIN") ? std::atoi(std::getenv("OCG_HBM_SPLITMIN")) : 96;
+  // eigenvalues per k_heev_bisect_split workgroup (RNT / split_spe threads each): 8, 16 or 32
+  int split_spe = [] {
+    const int v = std::getenv("OCG_HBM_SPLIT_SPE") ? std::atoi(std::getenv("OCG_HBM_SPLIT_SPE")) : 16;
+    return (v == 8 || v == 16 || v == 32) ? v : 16;
+  }();
+  // shifts per thread and multisection round (EProb::ks): 1 = bisection (default), 4 = round 5's
+  int bisect_ks = std::getenv("OCG_HBM_BISECT_KS") && std::atoi(std::getenv("OCG_HBM_BISECT_KS")) == 4 ? 4 : 1;
+  long split_launches = 0, split_blocks = 0;
   double phase_ms[8] = {0};
   long phase_n[8] = {0};
   double steps_done[8] = {0};
@@ -855,6 +867,7 @@ struct Engine {
         P.Z = walloc<double>(size_t(n) * n);
         P.Dv = walloc<double>(size_t(n) * n);
         P.kept = R.d_kept + pi;
+        P.ks = bisect_ks;
         R.probs.push_back(P);
         R.prob_job.push_back(int(j));
         R.prob_q.push_back(q);
@@ -925,6 +938,21 @@ struct Engine {
         if (any) thr_items.push_back(int(j));
       }
     }
+    // large register-path blocks: the tridiagonal in k_heev_vals_any, the
+    // eigenvalues split over workgroups (k_heev_bisect_split) right after it
+    std::vector<int> split;
+    int max_split = 0;
+    if (!thresh_on && split_min > 0)
+      for (int i = 0; i < np; ++i) {
+        const int n = R.probs[i].n;
+        const bool other = (coop_on && n >= std::max(coop_min, 65) && n <= CPT) ||
+                           (n >= std::max(big_min, 2) && n <= kBigMax) || (small_split && n <= kSmallMax);
+        if (!other && n >= std::max(split_min, reg_min) && n <= RNMAX) {
+          R.probs[i].defer = 1;
+          split.push_back(i);
+          max_split = std::max(max_split, n);
+        }
+      }
     R.d_probs = upload(R.probs);
     // bounds: device copy, then point the items at it
     const int* d_bounds = upload(bounds);
@@ -995,6 +1023,18 @@ struct Engine {
         hipLaunchKernelGGL(k_heev_vals_any, dim3(int(order.size())), dim3(RNT), lds_v, st, R.d_probs, upload(order),
                            reg_min);
         HCK(hipGetLastError());
+      }
+      if (!split.empty()) {
+        std::vector<int2> tasks;
+        for (int i : split)
+          for (int c = 0; split_spe * c < R.probs[i].n; ++c) tasks.push_back(make_int2(i, c));
+        hipLaunchKernelGGL(k_heev_bisect_split, dim3(int(tasks.size())), dim3(RNT), bisect_split_lds_bytes(max_split),
+                           st, R.d_probs, upload(tasks), split_spe);
+        hipLaunchKernelGGL(k_heev_bisect_fill, dim3(int(split.size())), dim3(RNT), bisect_split_lds_bytes(max_split),
+                           st, R.d_probs, upload(split));
+        HCK(hipGetLastError());
+        ++split_launches;
+        split_blocks += long(split.size());
       }
       if (!thr_items.empty()) {
         // the boundary counts read every sector's tridiagonal, the blocked kernel's too

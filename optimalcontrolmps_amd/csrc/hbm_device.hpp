@@ -328,6 +328,9 @@ struct EProb {
   // 1: the register kernel leaves the eigenvalues to k_heev_bisect, after
   // k_heev_thresh has raised thr_rel to the decomposition's Maxm boundary
   int defer;
+  // shifts per thread and multisection round (bisect_all / multisect): 1 (plain
+  // bisection, the default) or 4 (OCG_HBM_BISECT_KS=4)
+  int ks;
 };
 
 template <class T>

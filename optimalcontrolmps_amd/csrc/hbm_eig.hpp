@@ -100,13 +100,98 @@ __device__ __forceinline__ void sturm_count4(const double* d, const double* e2, 
   for (int t = 0; t < 4; ++t) cnt[t] = c[t];
 }
 
+// counts below KS shifts (sturm_count4's recurrence and guard for any KS)
+template <int KS>
+__device__ __forceinline__ void sturm_countk(const double* d, const double* e2, int n, const double* x,
+                                             double pivmin, int* cnt) {
+  double q[KS];
+  int c[KS];
+#pragma unroll
+  for (int t = 0; t < KS; ++t) {
+    q[t] = d[0] - x[t];
+    if (fabs(q[t]) < pivmin) q[t] = -pivmin;
+    c[t] = q[t] < 0 ? 1 : 0;
+  }
+  int i = 1;
+  for (; i + 3 < n; i += 4) {
+    double dv[4], ev[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { dv[u] = d[i + u]; ev[u] = e2[i + u - 1]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        q[t] = sturm_next(dv[u] - x[t], ev[u], q[t]);
+        if (fabs(q[t]) < pivmin) q[t] = -pivmin;
+        c[t] += q[t] < 0 ? 1 : 0;
+      }
+  }
+  for (; i < n; ++i) {
+    const double di = d[i], ei = e2[i - 1];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      q[t] = sturm_next(di - x[t], ei, q[t]);
+      if (fabs(q[t]) < pivmin) q[t] = -pivmin;
+      c[t] += q[t] < 0 ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < KS; ++t) cnt[t] = c[t];
+}
+// Multisection of the eigenvalues te = t0 .. t0 + ne - 1 (descending) of the
+// resolved ones: g = NTH / ne threads per eigenvalue (NTH / SPE in the split
+// kernel), KS shifts per thread, so KS g + 1 sub-intervals per round.  One
+// thread per eigenvalue and one shift (KS = 1, plain bisection) does the least
+// Sturm work per digit (rounds x shifts: 50 x 1 against 22 x 4), and at one
+// wave per SIMD the sequences are issue-bound, so it is the fastest choice.
+template <int KS, int NTH>
+__device__ __forceinline__ void multisect(const double* Ld, const double* Le2, int n, double gl0, double gu,
+                                          double atol, double pivmin, int t0, int ne, int g, double* w, double* lo,
+                                          double* hi, int* cnt) {
+  const int tid = threadIdx.x;
+  const double eps = 2.220446049250313e-16;
+  const int t = tid / g, s = tid - t * g, te = t0 + t;
+  const int np = KS * g + 1;  // sub-intervals per round
+  __syncthreads();
+  for (int tt = tid; tt < ne; tt += NTH) { lo[tt] = gl0; hi[tt] = gu; }
+  __syncthreads();
+  for (int it = 0; it < 256; ++it) {
+    bool active = false;
+    if (t < ne) {
+      const double l = lo[t], h = hi[t];
+      active = h - l > atol + 2.0 * eps * fmax(fabs(l), fabs(h));
+      if (active) {
+        double x[KS];
+#pragma unroll
+        for (int q = 0; q < KS; ++q) x[q] = l + (h - l) * double(KS * s + q + 1) / np;
+        sturm_countk<KS>(Ld, Le2, n, x, pivmin, cnt + KS * tid);
+      }
+    }
+    if (!__syncthreads_or(active)) break;
+    if (t < ne && s == 0 && active) {
+      const int idx = n - 1 - te;  // ascending index of the te-th largest
+      const double l = lo[t], h = hi[t];
+      double nl = l, nh = h;
+      for (int q = 1; q < np; ++q) {
+        const double x = l + (h - l) * double(q) / np;
+        if (cnt[KS * (t * g) + q - 1] > idx) { nh = x; break; }
+        nl = x;
+      }
+      lo[t] = nl;
+      hi[t] = nh;
+    }
+    __syncthreads();
+  }
+  for (int tt = tid; tt < ne; tt += NTH) w[t0 + tt] = 0.5 * (lo[tt] + hi[tt]);
+}
+
 // All eigenvalues (descending) of a real symmetric tridiagonal held in LDS
 // (Ld, Le2 = e^2), by multisection: g = NTH / n threads per eigenvalue, each
 // evaluating four Sturm counts per round (LAPACK dstebz bounds / tolerances).
 // Work arrays in LDS: lo, hi (n), cnt (4 * NTH ints).
 template <int NTH>
 __device__ __forceinline__ void bisect_all(const double* Ld, const double* Le2, int n, double thr_rel, double* w,
-                                           double* lo, double* hi, int* cnt) {
+                                           double* lo, double* hi, int* cnt, int ks = 4) {
   const int tid = threadIdx.x;
   __shared__ double bb[4][NTH / 64];
   __shared__ int sres;
@@ -152,6 +237,12 @@ __device__ __forceinline__ void bisect_all(const double* Ld, const double* Le2, 
   __syncthreads();
   const int nres = sres;
   // resolved eigenvalues (the nres largest) in rounds of NTH
+  if (ks == 1) {  // uniform (EProb::ks)
+    for (int t0 = 0; t0 < nres; t0 += NTH) {
+      const int ne = nres - t0 < NTH ? nres - t0 : NTH;
+      multisect<1, NTH>(Ld, Le2, n, nres < n ? fmax(gl, thr) : gl, gu, atol, pivmin, t0, ne, NTH / ne, w, lo, hi, cnt);
+    }
+  } else
   for (int t0 = 0; t0 < nres; t0 += NTH) {
     const int ne = nres - t0 < NTH ? nres - t0 : NTH;
     const int g = NTH / ne;  // threads per eigenvalue
@@ -455,7 +546,7 @@ __device__ __forceinline__ void heev_vals_reg_body(const EProb& P, char* smem) {
   double* hi = lo + NM;
   int* cnt = (int*)(hi + NM);
 #ifndef HBM_NO_BISECT  // timing builds of tools/eig_bench only
-  if (!P.defer) bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt);
+  if (!P.defer) bisect_all<RNT>(sd, se2, n, P.thr_rel, P.w, lo, hi, cnt, P.ks);
 #endif
 }
 
@@ -719,9 +810,129 @@ __global__ __launch_bounds__(BSN) void k_heev_bisect(const EProb* __restrict__ p
     Le2[i] = P.e[i] * P.e[i];
   }
   __syncthreads();
-  bisect_all<BSN>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt);
+  bisect_all<BSN>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt, P.ks);
 }
 __host__ __device__ constexpr int bisect_lds_bytes(int n) { return 4 * n * 8 + 4 * BSN * 4 + 64; }
+
+// ------------------------------------------------- split multisection (large blocks)
+// A block's multisection inside k_heev_vals_any gives one thread (four shifts)
+// to each eigenvalue once n > RNT / 2: 22 rounds of n-step Sturm sequences on
+// one CU, 32 % of the kernel at n = 192, while the launch's other CUs have long
+// finished their smaller blocks.  Blocks of order >= the split threshold are
+// marked defer (the register kernel stops after the tridiagonal) and their
+// eigenvalues are resolved here by ceil(n / SPE) workgroups each: SPE
+// eigenvalues per workgroup, RNT / SPE = 8 threads (33 shifts) per eigenvalue,
+// 10 rounds instead of 22.  Same bounds, tolerances and unresolved threshold as
+// bisect_all (every workgroup of a block computes them identically); the
+// unresolved eigenvalues' mean needs all resolved ones, so k_heev_bisect_fill
+// sets it afterwards.
+constexpr int SPE = 32;  // the largest chunk (split_spe: eigenvalues per workgroup, a divisor of RNT)
+// bounds, tolerances and the number of resolved eigenvalues of (Ld, Le2) (uniform)
+struct BisectBounds {
+  double gl, gu, pivmin, atol, tr, thr;
+  int nres;
+};
+template <int NTH>
+__device__ __forceinline__ BisectBounds bisect_bounds(const double* Ld, const double* Le2, int n, double thr_rel) {
+  const int tid = threadIdx.x;
+  __shared__ double bb[4][NTH / 64];
+  __shared__ int sres;
+  double gl = 1e300, gu = -1e300, emax = 0, tr = 0;
+  for (int i = tid; i < n; i += NTH) {
+    const double el = i > 0 ? sqrt(Le2[i - 1]) : 0.0, er = i + 1 < n ? sqrt(Le2[i]) : 0.0;
+    gl = fmin(gl, Ld[i] - el - er);
+    gu = fmax(gu, Ld[i] + el + er);
+    emax = fmax(emax, Le2[i]);
+    tr += Ld[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    gl = fmin(gl, __shfl_xor(gl, o, 64));
+    gu = fmax(gu, __shfl_xor(gu, o, 64));
+    emax = fmax(emax, __shfl_xor(emax, o, 64));
+    tr += __shfl_xor(tr, o, 64);
+  }
+  if ((tid & 63) == 0) { bb[0][tid >> 6] = gl; bb[1][tid >> 6] = gu; bb[2][tid >> 6] = emax; bb[3][tid >> 6] = tr; }
+  __syncthreads();
+  gl = bb[0][0]; gu = bb[1][0]; emax = bb[2][0]; tr = bb[3][0];
+  for (int i = 1; i < NTH / 64; ++i) {
+    gl = fmin(gl, bb[0][i]); gu = fmax(gu, bb[1][i]); emax = fmax(emax, bb[2][i]); tr += bb[3][i];
+  }
+  const double eps = 2.220446049250313e-16, safmin = 2.2250738585072014e-308;
+  const double tnorm = fmax(fabs(gl), fabs(gu));
+  BisectBounds B;
+  B.pivmin = safmin * fmax(1.0, emax);
+  B.gl = gl - (2.0 * eps * tnorm * n + 2.0 * B.pivmin);
+  B.gu = gu + (2.0 * eps * tnorm * n + 2.0 * B.pivmin);
+  B.atol = 4.0 * eps * tnorm;
+  B.tr = tr;
+  B.thr = thr_rel * tr;
+  if (tid == 0) {
+    int below = 0;
+    if (B.thr > 0) {
+      double x[4] = {B.thr, B.thr, B.thr, B.thr};
+      int c4[4];
+      sturm_count4(Ld, Le2, n, x, B.pivmin, c4);
+      below = c4[0];
+    }
+    sres = n - below;
+  }
+  __syncthreads();
+  B.nres = sres;
+  return B;
+}
+// problem t.x, eigenvalues [SPE t.y, SPE t.y + SPE) of the resolved ones (descending)
+__global__ __launch_bounds__(RNT) void k_heev_bisect_split(const EProb* __restrict__ probs,
+                                                           const int2* __restrict__ tasks, int spe) {
+  extern __shared__ __align__(16) char smem_sp[];
+  const int2 tk = tasks[blockIdx.x];
+  const EProb P = probs[tk.x];
+  const int n = P.n, tid = threadIdx.x;
+  double* Ld = reinterpret_cast<double*>(smem_sp);
+  double* Le2 = Ld + n;
+  __shared__ double lo[SPE], hi[SPE];
+  __shared__ int cnt[4 * RNT];
+  for (int i = tid; i < n; i += RNT) {
+    Ld[i] = P.d[i];
+    Le2[i] = P.e[i] * P.e[i];
+  }
+  __syncthreads();
+  const BisectBounds B = bisect_bounds<RNT>(Ld, Le2, n, P.thr_rel);
+  const int t0 = spe * tk.y;
+  if (t0 >= B.nres) return;  // uniform
+  const int ne = B.nres - t0 < spe ? B.nres - t0 : spe;
+  const double gl0 = B.nres < n ? fmax(B.gl, B.thr) : B.gl;
+  // RNT / spe threads per eigenvalue (also when ne < spe: the same points)
+  if (P.ks == 1) multisect<1, RNT>(Ld, Le2, n, gl0, B.gu, B.atol, B.pivmin, t0, ne, RNT / spe, P.w, lo, hi, cnt);
+  else multisect<4, RNT>(Ld, Le2, n, gl0, B.gu, B.atol, B.pivmin, t0, ne, RNT / spe, P.w, lo, hi, cnt);
+}
+__host__ __device__ constexpr int bisect_split_lds_bytes(int n) { return 16 * n + 64; }
+// the unresolved eigenvalues of a split problem: their mean (trace minus the
+// resolved ones), as bisect_all sets them; one workgroup per problem
+__global__ __launch_bounds__(RNT) void k_heev_bisect_fill(const EProb* __restrict__ probs,
+                                                          const int* __restrict__ idx) {
+  extern __shared__ __align__(16) char smem_fl[];
+  const EProb P = probs[idx[blockIdx.x]];
+  const int n = P.n, tid = threadIdx.x;
+  double* Ld = reinterpret_cast<double*>(smem_fl);
+  double* Le2 = Ld + n;
+  __shared__ double bb[RNT / 64];
+  for (int i = tid; i < n; i += RNT) {
+    Ld[i] = P.d[i];
+    Le2[i] = P.e[i] * P.e[i];
+  }
+  __syncthreads();
+  const BisectBounds B = bisect_bounds<RNT>(Ld, Le2, n, P.thr_rel);
+  if (B.nres >= n) return;  // uniform
+  double sr = 0;
+  for (int t = tid; t < B.nres; t += RNT) sr += P.w[t];
+  for (int o = 32; o > 0; o >>= 1) sr += __shfl_xor(sr, o, 64);
+  if ((tid & 63) == 0) bb[tid >> 6] = sr;
+  __syncthreads();
+  sr = 0;
+  for (int i = 0; i < RNT / 64; ++i) sr += bb[i];
+  const double mean = fmin(fmax((B.tr - sr) / (n - B.nres), 0.0), B.thr);
+  for (int t = B.nres + tid; t < n; t += RNT) P.w[t] = mean;
+}
 
 // One launch per decomposition: each workgroup picks the variant for its
 // block's order (register slot grid 2 / 4 / 8 / 12 / 13, or the LDS / L2
@@ -1660,7 +1871,7 @@ __device__ __forceinline__ void vals_big_body(const EProb& P) {
   double* lo = reinterpret_cast<double*>(ws);
   double* hi = lo + kBigMax;
   int* cnt = reinterpret_cast<int*>(hi + kBigMax);
-  bisect_all<VBG>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt);
+  bisect_all<VBG>(Ld, Le2, n, P.thr_rel, P.w, lo, hi, cnt, P.ks);
 #ifdef HBM_STAMP
   __syncthreads();
   STAMP(6);

@@ -135,6 +135,31 @@ def _decomp_env(monkeypatch, env, Ms, cutoff, maxm):
     return res, st
 
 
+def test_split_multisection_vs_numpy_and_in_kernel(monkeypatch):
+    """register-path blocks of order >= 96 (config 4's largest sectors) leave
+    their eigenvalues to k_heev_bisect_split / k_heev_bisect_fill (32 per
+    workgroup, 8 threads each): against numpy, and against the in-kernel
+    multisection (OCG_HBM_SPLITMIN=0) to rounding, including a rank-deficient
+    block (unresolved eigenvalues below the threshold: the fill kernel's mean)
+    and a degenerate cluster; orders below the threshold stay in-kernel"""
+    rng = np.random.default_rng(96)
+    spec = np.exp(-np.arange(160) / 6.0)
+    spec[4:9] = spec[4]
+    Ms = [block(rng, 96, 130, np.exp(-np.arange(96) / 5.0)),
+          block(rng, 150, 170, np.exp(-np.arange(60) / 4.0), rank=60),
+          block(rng, 160, 160, spec),
+          block(rng, 192, 230, 1.0 / (1.0 + np.arange(192)) ** 1.5),
+          block(rng, 208, 208, np.exp(-np.arange(208) / 9.0)),
+          block(rng, 64, 80, np.exp(-np.arange(64) / 3.0))]
+    for maxm in (512, 70):
+        res, _ = _decomp_env(monkeypatch, {}, Ms, 1e-8, maxm)
+        ref, _ = _decomp_env(monkeypatch, {"OCG_HBM_SPLITMIN": "0"}, Ms, 1e-8, maxm)
+        for M, r, r0 in zip(Ms, res, ref):
+            check(M, r, 1e-8, maxm)
+            assert r[0] == r0[0]
+            assert np.abs(r[2] @ r[3] - r0[2] @ r0[3]).max() <= 1e-11 * np.abs(r0[2] @ r0[3]).max()
+
+
 def test_coop_members_bitwise_and_vs_one_cu(monkeypatch):
     """k_heev_vals_coop (hbm_coop.hpp): the multi-CU reduction gives the same
     bits whatever the number G of workgroups per block (1, 3, 8, 16: the

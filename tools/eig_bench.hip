@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
     p.A = dA + nn * b; p.U = dU + nn * b; p.ph = dph + n * b;
     p.d = dd + n * b; p.e = de + n * b; p.tau = dtau + (n + 64) * b; p.w = dw + n * b;
     p.Z = dZ + nn * b; p.Dv = dDv + nn * b; p.n = n; p.q = 0; p.kept = dkept + b; p.thr_rel = thr_rel;
+    p.ks = getenv("EIG_KS") ? atoi(getenv("EIG_KS")) : 1;  // shifts per multisection thread
   }
   EProb* dP;
   CK(hipMalloc(&dP, sizeof(EProb) * B));
