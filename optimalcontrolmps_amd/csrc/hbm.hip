@@ -265,6 +265,8 @@ struct Engine {
   // shifts per thread and multisection round (EProb::ks): 1 = bisection (default), 4 = round 5's
   int bisect_ks = std::getenv("OCG_HBM_BISECT_KS") && std::atoi(std::getenv("OCG_HBM_BISECT_KS")) == 4 ? 4 : 1;
   long split_launches = 0, split_blocks = 0;
+  // the split runs while its workgroups number at most split_max_wg per CU (OCG_HBM_SPLIT_WG)
+  int split_max_wg = std::getenv("OCG_HBM_SPLIT_WG") ? std::atoi(std::getenv("OCG_HBM_SPLIT_WG")) : 2;
   double phase_ms[8] = {0};
   long phase_n[8] = {0};
   double steps_done[8] = {0};
@@ -940,19 +942,26 @@ struct Engine {
     }
     // large register-path blocks: the tridiagonal in k_heev_vals_any, the
     // eigenvalues split over workgroups (k_heev_bisect_split) right after it
+    // Only while the split's workgroups fit about two per CU: a launch with many
+    // large blocks (the full-horizon row batches) already fills the GPU, and the
+    // split's g threads per eigenvalue would only add Sturm work there.
     std::vector<int> split;
     int max_split = 0;
-    if (!thresh_on && split_min > 0)
+    if (!thresh_on && split_min > 0) {
+      long ntask = 0;
       for (int i = 0; i < np; ++i) {
         const int n = R.probs[i].n;
         const bool other = (coop_on && n >= std::max(coop_min, 65) && n <= CPT) ||
                            (n >= std::max(big_min, 2) && n <= kBigMax) || (small_split && n <= kSmallMax);
         if (!other && n >= std::max(split_min, reg_min) && n <= RNMAX) {
-          R.probs[i].defer = 1;
           split.push_back(i);
           max_split = std::max(max_split, n);
+          ntask += (n + split_spe - 1) / split_spe;
         }
       }
+      if (ntask > long(split_max_wg) * n_cu) split.clear();
+      for (int i : split) R.probs[i].defer = 1;
+    }
     R.d_probs = upload(R.probs);
     // bounds: device copy, then point the items at it
     const int* d_bounds = upload(bounds);

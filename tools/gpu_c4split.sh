@@ -1,10 +1,8 @@
-# c4rows A/B of the split multisection: chunk size and threshold
+# c4rows A/B of the split multisection (OCG_HBM_SPLIT_WG: workgroups per CU it may use; SPLITMIN=0: off)
 set -o pipefail
 mkdir -p gpurun_out
 B="python bench.py --workload c4rows --steps 2 --warmup 1 --no-cpu-baseline --state-cache /tmp/c4s.npz"
-timeout -k 10 200 $B > gpurun_out/c4_s16_96.json 2> /dev/null || exit 1
-OCG_HBM_SPLIT_SPE=8 timeout -k 10 200 $B > gpurun_out/c4_s8_96.json 2> /dev/null || exit 1
-OCG_HBM_SPLIT_SPE=32 timeout -k 10 200 $B > gpurun_out/c4_s32_96.json 2> /dev/null || exit 1
-OCG_HBM_SPLITMIN=64 timeout -k 10 200 $B > gpurun_out/c4_s16_64.json 2> /dev/null || exit 1
-OCG_HBM_SPLITMIN=48 OCG_HBM_SPLIT_SPE=8 timeout -k 10 200 $B > gpurun_out/c4_s8_48.json 2> /dev/null || exit 1
-timeout -k 10 200 $B > gpurun_out/c4_s16_96b.json 2> /dev/null || exit 1
+for cfg in "OCG_HBM_SPLIT_WG=2" "OCG_HBM_SPLIT_WG=1000" "OCG_HBM_SPLITMIN=0" "OCG_HBM_SPLIT_WG=4" "OCG_HBM_SPLIT_WG=2"; do
+  env $cfg timeout -k 10 200 $B > gpurun_out/c4ab_tmp.json 2> /dev/null || exit 1
+  python -c "import json,sys; d=json.loads(open('gpurun_out/c4ab_tmp.json').read().strip().splitlines()[-1]); print('$cfg', round(d['ms_per_step'],1), round(d['single_chain_steps_per_sec'],2))" >> gpurun_out/c4ab.txt
+done
