@@ -809,15 +809,15 @@ def bench_c4(args):
             # the sample's parts (hbm timers: kind 3 = the row batches of the two-phase path). The
             # rows of a sample run in smaller lockstep batches than the whole Hessian's (32 rows vs
             # 799 joining over the horizon), so their row-step rate is a lower bound of the whole
-            # run's; the whole getHessian is not priced from it (measured whole: 359-366 s, r04/r05)
+            # run's; the whole getHessian is not priced from it (measured whole: 357.6 s, r06)
             rows_ms = eng.stats(3)["ms"] / args.steps
             res["horizon_sample"] = {
                 "rows": R, "of_rows": Nt - 2, "row_steps": row_steps, "of_row_steps": (Nt - 2) * (Nt - 3) // 2,
                 "precompute_ms": 1e3 * elapsed / args.steps - rows_ms, "rows_ms": rows_ms,
                 "row_steps_per_s": row_steps / max(rows_ms * 1e-3, 1e-9),
-                "whole_getHessian_measured_s": [359, 366],
-                "whole_source": "profiles/r04_bench_c4full_prio.json, profiles/r05_bench_c4full_profiled.json "
-                                "(same config-4 code path: the multi-CU eigensolver serves orders >= 209 only)"}
+                "whole_getHessian_measured_s": 357.6,
+                "whole_source": "profiles/r06_bench_c4full.json (round 6 code: one GPU, the two-phase path; "
+                                "rounds 4-5: 359-366 s, profiles/r04_bench_c4full_prio.json)"}
         res["env"] = run_env()
         if world == 1 and not args.no_cpu_baseline and not grad and not args.profiled:
             res["cpu_baseline"] = (cpu_baseline_c5(ini, Nt, args.cpu_threads) if c5 else
