@@ -988,21 +988,29 @@ constexpr int kVecLds = 143360;  // bytes of the Z + pivot / Gram / reflector-bl
 // global: pivots by a refined reciprocal, the forward and backward sweeps
 // unrolled by 4 with their loads issued ahead of the dependent FMA chain (few
 // threads carry the whole batch: nothing else hides the memory latency).
+#ifndef INVIT_ITERS
+#define INVIT_ITERS 2  // inverse-iteration sweeps per eigenvalue (3 until round 6: the same residuals, tools/gpu_invit.sh)
+#endif
 __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const double* __restrict__ Le, int n,
                                            double lam, double tiny, double* __restrict__ Z, int ldz, int jz,
                                            double* __restrict__ Dv, int ldd, int jd, int jj) {
+  // LDL^T of T - lam I; Dv keeps the pivots' reciprocals 1 / q_i (a refined
+  // hardware reciprocal, computed once here), so neither sweep divides
+  auto rcpr = [](double q) {
+    double r = __builtin_amdgcn_rcp(q);
+    return fma(r, fma(-q, r, 1.0), r);
+  };
   double q = Ld[0] - lam;
   if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
-  Dv[jd] = q;
   for (int i = 1; i < n; ++i) {
-    double r = __builtin_amdgcn_rcp(q);
-    r = fma(r, fma(-q, r, 1.0), r);
+    const double r = rcpr(q);
+    Dv[(size_t)(i - 1) * ldd + jd] = r;
     q = fma(-Le[i - 1] * Le[i - 1], r, Ld[i] - lam);
     if (fabs(q) < tiny) q = q < 0 ? -tiny : tiny;
-    Dv[(size_t)i * ldd + jd] = q;
   }
+  Dv[(size_t)(n - 1) * ldd + jd] = rcpr(q);
   for (int i = 0; i < n; ++i) Z[(size_t)i * ldz + jz] = hrand(i, jj);
-  for (int it = 0; it < 3; ++it) {
+  for (int it = 0; it < INVIT_ITERS; ++it) {
     // forward: y_i = b_i - (e_{i-1} / q_{i-1}) y_{i-1}
     double y = Z[jz];
     int i = 1;
@@ -1011,7 +1019,7 @@ __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const 
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         b[t] = Z[(size_t)(i + t) * ldz + jz];
-        l[t] = Le[i + t - 1] / Dv[(size_t)(i + t - 1) * ldd + jd];
+        l[t] = Le[i + t - 1] * Dv[(size_t)(i + t - 1) * ldd + jd];
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1020,11 +1028,11 @@ __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const 
       }
     }
     for (; i < n; ++i) {
-      y = fma(-Le[i - 1] / Dv[(size_t)(i - 1) * ldd + jd], y, Z[(size_t)i * ldz + jz]);
+      y = fma(-Le[i - 1] * Dv[(size_t)(i - 1) * ldd + jd], y, Z[(size_t)i * ldz + jz]);
       Z[(size_t)i * ldz + jz] = y;
     }
     // backward: x_i = (y_i - e_i x_{i+1}) / q_i
-    double xn = Z[(size_t)(n - 1) * ldz + jz] / Dv[(size_t)(n - 1) * ldd + jd];
+    double xn = Z[(size_t)(n - 1) * ldz + jz] * Dv[(size_t)(n - 1) * ldd + jd];
     Z[(size_t)(n - 1) * ldz + jz] = xn;
     double ss = xn * xn;
     i = n - 2;
@@ -1034,7 +1042,7 @@ __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const 
       for (int t = 0; t < 4; ++t) {
         b[t] = Z[(size_t)(i - t) * ldz + jz];
         e[t] = Le[i - t];
-        rq[t] = 1.0 / Dv[(size_t)(i - t) * ldd + jd];
+        rq[t] = Dv[(size_t)(i - t) * ldd + jd];
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -1044,7 +1052,7 @@ __device__ __forceinline__ void invit_fast(const double* __restrict__ Ld, const 
       }
     }
     for (; i >= 0; --i) {
-      xn = (Z[(size_t)i * ldz + jz] - Le[i] * xn) / Dv[(size_t)i * ldd + jd];
+      xn = (Z[(size_t)i * ldz + jz] - Le[i] * xn) * Dv[(size_t)i * ldd + jd];
       Z[(size_t)i * ldz + jz] = xn;
       ss = fma(xn, xn, ss);
     }
