@@ -48,6 +48,7 @@ struct OcgParams {
   const int* oplan;         // overlap plan of the padded layout (fast_overlap.hpp), or null: the
                             // row overlaps of getHessian run on the general contraction
   int ovl_bytes;            // LDS of the padded overlap (k_row_overlaps_pad; <= fast_off)
+  int ovl_dh_bytes;         // LDS of the padded <x|y> / <x|dH|y> pairs (k_overlaps_pad)
 };
 #define OCG_ERR_JACOBI 1
 #define OCG_ERR_WATCHDOG 2

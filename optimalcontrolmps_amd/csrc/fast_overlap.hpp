@@ -29,13 +29,16 @@ struct FastOverlap {
   const bool act;  // wave 0
   LDS int *PL, *DX, *DY, *BX, *BY;
   lzp XP, YP, T, E0, E1;
+  lzp T1, F0, F1;  // <X|dH|Y> (contract_dH): T of the dH environment, its two environments
+  bool dh = false;
   int L, Q1, p, np, nblk, nsq;
   int zs, ze;  // zero slots of T and of both environments (XP's and YP's: np)
   int o_d, o_eo, o_en, o_po, o_sb, o_elo, o_el, o_ls, o_blk;
 
   // base: LDS of overlap_lds_bytes(plan) bytes, 16-byte aligned
-  __device__ OCG_INLINE FastOverlap(const OcgParams& P, char* base, const int* gplan)
-      : lane(threadIdx.x & 63), act(threadIdx.x < 64) {
+  // with_dH: the dH buffers after the others (overlap_lds_bytes(plan, P, true))
+  __device__ OCG_INLINE FastOverlap(const OcgParams& P, char* base, const int* gplan, bool with_dH = false)
+      : lane(threadIdx.x & 63), act(threadIdx.x < 64), dh(with_dH) {
     using namespace fastp;
     if (!gplan) return;
     // the header is read from global memory (uniform scalar loads)
@@ -57,6 +60,9 @@ struct FastOverlap {
     T = YP + (np + 2);
     E0 = T + (zs + 2);
     E1 = E0 + (ze + 2);
+    T1 = E1 + (ze + 2);
+    F0 = T1 + (zs + 2);
+    F1 = F0 + (ze + 2);
   }
   __device__ __forceinline__ void wsync() const {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -75,6 +81,11 @@ struct FastOverlap {
       T[zs] = c2(0.0, 0.0);
       E0[ze] = c2(0.0, 0.0);
       E1[ze] = c2(0.0, 0.0);
+      if (dh) {
+        T1[zs] = c2(0.0, 0.0);
+        F0[ze] = c2(0.0, 0.0);
+        F1[ze] = c2(0.0, 0.0);
+      }
     }
     wsync();
   }
@@ -220,6 +231,93 @@ struct FastOverlap {
       En = t;
     }
     return Ep[0];
+  }
+
+  // <X|dH|Y>, dH = sum_k 0.5 n_k (n_k - 1) (propagatorDeriv, src/BH_tDMRG.cpp:10-14;
+  // Chain::overlap's with_dH): E carries the identity string, F the strings with
+  // dH already applied, F_k = sum_n X^H (F_(k-1) Y + f(n) E_(k-1) Y), f = P.dH.
+  // Per n the two partial sums s0, s1 first, as Chain::overlap adds them.
+  __device__ OCG_INLINE zc contract_dH(lzp Y, const double* fdh) {
+    using fastp::kMaxDm;
+    using fastp::kOvMaxP;
+    if (!act) return c2(0.0, 0.0);
+    if (lane == 0) {
+      E0[0] = c2(1.0, 0.0);
+      F0[0] = c2(0.0, 0.0);
+    }
+    wsync();
+    lzp Ep = E0, En = E1, Fp = F0, Fn = F1;
+    for (int k = 1; k <= L; ++k) {
+      const int s0 = PL[o_sb + k], ns = PL[o_sb + k + 1] - s0;
+      for (int e = lane; e < ns; e += 64) {
+        const int w = PL[o_ls + 4 * (s0 + e) + 2];
+        const int a = w & 15, c = (w >> 4) & 15, dq = (w >> 8) & 15, dr = (w >> 12) & 15, eo = unsigned(w) >> 16;
+        const int yb = s0 + e - a * dr, eb = eo + a * dq;
+        zc ev[kMaxDm], fv[kMaxDm], yv[kMaxDm];
+#pragma unroll
+        for (int t = 0; t < kMaxDm; ++t) {
+          ev[t] = Ep[t < dq ? eb + t : ze];
+          fv[t] = Fp[t < dq ? eb + t : ze];
+          yv[t] = Y[t < dq ? yb + t * dr : np];
+        }
+        zc a0 = c2(0.0, 0.0), a1 = c2(0.0, 0.0);
+#pragma unroll
+        for (int t = 0; t < kMaxDm; ++t) {
+          cacc(a0, ev[t], yv[t]);
+          cacc(a1, fv[t], yv[t]);
+        }
+        T[e] = a0;
+        T1[e] = a1;
+      }
+      wsync();
+      const int ne = PL[o_en + k], el0 = PL[o_elo + k];
+      for (int x = lane; x < ne; x += 64) {
+        const int w = PL[o_el + el0 + x];
+        const int qp = w & 255, cp = (w >> 8) & 15, c = (w >> 12) & 15, dr = unsigned(w) >> 16;
+        int o[kOvMaxP], dq[kOvMaxP];
+#pragma unroll
+        for (int n = 0; n < kOvMaxP; ++n) {
+          const int q = qp - n;
+          const bool in = n < p && q >= 0;
+          const int on = PL[in ? o_po + (k * Q1 + q) * p + n : o_po];
+          const int dn = PL[in ? o_d + (k - 1) * Q1 + q : o_d];
+          o[n] = on;
+          dq[n] = (in && on >= 0) ? dn : 0;
+        }
+        zc acc0 = c2(0.0, 0.0), acc1 = c2(0.0, 0.0);
+#pragma unroll
+        for (int n = 0; n < kOvMaxP; ++n) {
+          if (n < p) {  // uniform
+            zc xv[kMaxDm], tv[kMaxDm], uv[kMaxDm];
+#pragma unroll
+            for (int a = 0; a < kMaxDm; ++a) {
+              const bool v = a < dq[n];
+              xv[a] = XP[v ? s0 + o[n] + cp + a * dr : np];
+              tv[a] = T[v ? o[n] + c + a * dr : zs];
+              uv[a] = T1[v ? o[n] + c + a * dr : zs];
+            }
+            zc p0 = c2(0.0, 0.0), p1 = c2(0.0, 0.0);
+#pragma unroll
+            for (int a = 0; a < kMaxDm; ++a) {
+              cjacc(p0, xv[a], tv[a]);
+              cjacc(p1, xv[a], uv[a]);
+            }
+            acc0 = cadd(acc0, p0);
+            acc1 = cadd(acc1, cadd(p1, cscale(p0, fdh[n])));
+          }
+        }
+        En[x] = acc0;
+        Fn[x] = acc1;
+      }
+      wsync();
+      lzp t = Ep;
+      Ep = En;
+      En = t;
+      t = Fp;
+      Fp = Fn;
+      Fn = t;
+    }
+    return Fp[0];
   }
 };
 

@@ -524,11 +524,13 @@ inline std::vector<int> build_overlap_plan(const OcgParams& P, const std::vector
 }
 // LDS of the one-wave overlap (fast_overlap.hpp): plan, two dims / block-offset
 // arrays, the two padded states and their zero slot, T, two environments
-inline int overlap_lds_bytes(const std::vector<int>& I, const OcgParams& P) {
+// (with_dH: the <X|dH|Y> buffers too, FastOverlap::contract_dH)
+inline int overlap_lds_bytes(const std::vector<int>& I, const OcgParams& P, bool with_dH = false) {
   using namespace ocg::fastp;
   auto al = [](int x) { return (x + 3) & ~3; };
   const int ints = I[kOvNint] + 2 * al(P.nsq) + 2 * al(I[kOvNblk] + 1);
-  const int zs = 2 * (I[kOvNp] + 2) + (I[kOvMaxSite] + 2) + 2 * (I[kOvMaxEn] + 2);
+  int zs = 2 * (I[kOvNp] + 2) + (I[kOvMaxSite] + 2) + 2 * (I[kOvMaxEn] + 2);
+  if (with_dH) zs += (I[kOvMaxSite] + 2) + 2 * (I[kOvMaxEn] + 2);
   return ints * 4 + zs * 16;
 }
 

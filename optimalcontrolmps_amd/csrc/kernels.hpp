@@ -136,6 +136,27 @@ __device__ OCG_INLINE void body_overlaps(char* smem, OcgParams P, const zc* gf, 
   flush_stats(c, stats, b, 8.0 * b / 16.0 * 4.0, 0.0);
 }
 
+// body_overlaps on the padded layout (fast_overlap.hpp, P.oplan set): one wave
+// per pair, grid-stride
+__device__ inline OCG_INLINE void body_overlaps_pad(char* smem, OcgParams P, Pool pool, const int* xs, const int* ys,
+                                                    int npairs, int with_dH, zc* out, double* stats) {
+  FastOverlap o(P, smem, P.oplan, true);
+  o.init(P.oplan);
+  double b = 0;
+  for (int i = blockIdx.x; i < npairs; i += gridDim.x) {
+    const int ny = o.load(SLOT_D(pool, P, xs[i]), SLOT_X(pool, P, xs[i]), SLOT_D(pool, P, ys[i]),
+                          SLOT_X(pool, P, ys[i]));
+    const zc r = with_dH ? o.contract_dH(o.YP, P.dH) : o.contract(o.YP);
+    b += 32.0 * ny;
+    if (threadIdx.x == 0) out[i] = r;
+    o.wsync();  // LDS reuse by the next pair
+  }
+  if (threadIdx.x == 0 && stats) {
+    atomicAdd(stats + 0, b);
+    atomicAdd(stats + 1, 8.0 * b / 16.0 * 4.0);
+  }
+}
+
 template <int NT>
 __device__ OCG_INLINE void body_apply_dH(char* smem, OcgParams P, const zc* gf, const zc* gb, const int* md,
                                                  Pool pool, const int* in, const int* outs, int n, double* norms,

@@ -112,6 +112,13 @@ __global__ __launch_bounds__(64) void k_row_overlaps_pad(OcgParams P, Pool pool,
   ocg::body_row_overlaps_pad(smem, P, pool, xih_base, rows, nrows, rbase, rs, rnorm, divT, F, N, H, stats, K, cs);
 }
 
+// <x|y> / <x|dH|y> pairs on the padded layout (fast_overlap.hpp): one wave per pair
+__global__ __launch_bounds__(64) void k_overlaps_pad(OcgParams P, Pool pool, const int* xs, const int* ys, int n,
+                                                     int with_dH, zc* out, double* stats) {
+  extern __shared__ __align__(16) char smem[];
+  ocg::body_overlaps_pad(smem, P, pool, xs, ys, n, with_dH, out, stats);
+}
+
 __global__ __launch_bounds__(NT) void k_steps(OcgParams P, const zc* gf, const zc* gb, const int* md,
                                               Pool pool, const int* slots, int n, const double* u, int u_stride,
                                               int nsteps, int forward, double* stats) {
@@ -544,6 +551,7 @@ static int finish_params(ocg_ctx* c) {
   c->P.fast_off = 0;
   c->P.oplan = nullptr;
   c->P.ovl_bytes = 0;
+  c->P.ovl_dh_bytes = 0;
   const char* nf = std::getenv("OCG_NO_FAST");
   if (nf && nf[0] && nf[0] != '0') {
     c->fast_why = "OCG_NO_FAST";
@@ -585,6 +593,7 @@ static int finish_params(ocg_ctx* c) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       c->P.oplan = c->d_oplan;
       c->P.ovl_bytes = ob;
+      c->P.ovl_dh_bytes = ocg_host::overlap_lds_bytes(ov, c->P, true);
       if (std::getenv("OCG_FAST_DUMP"))
         std::fprintf(stderr, "[fast ovl] np %d nblk %d ints %d bytes %d\n", ov[ocg::fastp::kOvNp],
                      ov[ocg::fastp::kOvNblk], ov[ocg::fastp::kOvNint], ob);
@@ -1041,6 +1050,20 @@ int ocg_step_batch(ocg_ctx* c, int n, const int* dims, const double* const* data
   return 0;
 }
 
+// n pairs <x|y> (with_dH: <x|dH|y>) of slot lists xs, ys (device) into out (device), on the
+// context's stream: the padded contraction when the context has its plan, else Chain::overlap
+static void ovl_pairs(ocg_ctx* c, const int* xs, const int* ys, int n, int with_dH, zc* out) {
+  if (n <= 0) return;
+  if (c->P.oplan) {
+    hipLaunchKernelGGL(k_overlaps_pad, dim3(unsigned(n)), dim3(64), c->P.ovl_dh_bytes, c->stream, c->P, c->pool, xs,
+                       ys, n, with_dH, out, c->d_stats + 1 * 3);
+    return;
+  }
+  const OcgParams Po = c->Po();
+  hipLaunchKernelGGL(k_overlaps, dim3(unsigned(n)), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md,
+                     c->pool, xs, ys, n, with_dH, out, c->d_stats + 1 * 3);
+}
+
 static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::vector<int>& ys, int with_dH,
                            std::vector<zc>& out) {
   const OcgParams& P = c->P;
@@ -1052,9 +1075,7 @@ static int launch_overlaps(ocg_ctx* c, const std::vector<int>& xs, const std::ve
   idx.insert(idx.end(), ys.begin(), ys.end());
   HIPCHK(c, hipMemcpyAsync(c->d_idx, idx.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, c->stream));
   if (int rc = begin_kernel(c)) return rc;
-  const OcgParams Pn = c->Po();
-  hipLaunchKernelGGL(k_overlaps, dim3(n), dim3(NT), Pn.lds_bytes, c->stream, Pn, c->d_gf, c->d_gb, c->d_md, c->pool,
-                     c->d_idx, c->d_idx + n, n, with_dH, c->d_c, c->d_stats + 1 * 3);
+  ovl_pairs(c, c->d_idx, c->d_idx + n, n, with_dH, c->d_c);
   if (int rc = end_kernel(c, 1)) return rc;
   out.resize(n);
   HIPCHK(c, hipMemcpyAsync(out.data(), c->d_c, sizeof(zc) * n, hipMemcpyDeviceToHost, c->stream));
@@ -1607,10 +1628,8 @@ static int hessian_fused(ocg_ctx* c, int K, const double* u, int N, const int* r
   HIPCHK(c, hipEventRecord(c->evh[1], c->stream));
   const OcgParams Po = c->Po();
   // divT of every control at d_pc[k N + i], F of control k at d_pc[K N + k]
-  hipLaunchKernelGGL(k_overlaps, dim3(K * N), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md,
-                     c->pool, c->d_idx, c->d_idx + K * N, K * N, 1, c->d_pc, c->d_stats + 1 * 3);
-  hipLaunchKernelGGL(k_overlaps, dim3(K), dim3(NT), Po.lds_bytes, c->stream, Po, c->d_gf, c->d_gb, c->d_md, c->pool,
-                     c->d_idx + 2 * K * N, c->d_idx + 2 * K * N + K, K, 0, c->d_pc + K * N, c->d_stats + 1 * 3);
+  ovl_pairs(c, c->d_idx, c->d_idx + K * N, K * N, 1, c->d_pc);
+  ovl_pairs(c, c->d_idx + 2 * K * N, c->d_idx + 2 * K * N + K, K, 0, c->d_pc + K * N);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->evh[2], c->stream));
   static const int rov_w = [] {  // A/B switch: OCG_ROWOV_WAVE=0 -> two-wave row overlaps

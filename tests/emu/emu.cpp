@@ -138,6 +138,7 @@ void* emu_new_ex(int L, int p, int Q, double J, double dt, double cutoff, int ma
   if (!e->oplan.empty() && ocg_host::overlap_lds_bytes(e->oplan, e->P) <= off && !(no && no[0] && no[0] != '0')) {
     e->P.oplan = e->oplan.data();
     e->P.ovl_bytes = ocg_host::overlap_lds_bytes(e->oplan, e->P);
+    e->P.ovl_dh_bytes = ocg_host::overlap_lds_bytes(e->oplan, e->P, true);
   }
   return e;
 }
@@ -183,6 +184,25 @@ void emu_overlap(void* h, const int* dx, const double* x, const int* dy, const d
   });
   out[0] = r.x;
   out[1] = r.y;
+}
+
+// the same pair on the padded contraction (fast_overlap.hpp; fast contexts only): 0, or -1 without the plan
+int emu_overlap_pad(void* h, const int* dx, const double* x, const int* dy, const double* y, int with_dH,
+                    double* out) {
+  Emu& e = *static_cast<Emu*>(h);
+  if (!e.P.oplan) return -1;
+  put(e, 2, dx, x);
+  put(e, 3, dy, y);
+  int xs = 2, ys = 3;
+  ocg::zc r = ocg::c2(0, 0);
+  OcgParams P = e.P;
+  const int lds = e.lds;
+  e.lds = std::max(e.lds, P.ovl_dh_bytes);
+  launch(e, 1, [&](char* smem) { ocg::body_overlaps_pad(smem, P, e.pool(), &xs, &ys, 1, with_dH, &r, e.stats + 3); });
+  e.lds = lds;
+  out[0] = r.x;
+  out[1] = r.y;
+  return 0;
 }
 
 // full getHessian pipeline (GRAPE, no regularisation): H (N*N), divT (2N), F (2), fid (N)

@@ -24,6 +24,7 @@ def lib():
         if hasattr(L, "emu_hessian_fused"):  # absent from the steps-only sanitizer build
             L.emu_hessian_fused.argtypes = [C.c_void_p, ip, dp, ip, dp, dp, C.c_int, dp, dp, dp]
             L.emu_hessian.argtypes = [C.c_void_p, ip, dp, ip, dp, dp, C.c_int, dp, dp, dp, dp, C.c_int]
+            L.emu_overlap_pad.argtypes = [C.c_void_p, ip, dp, ip, dp, C.c_int, dp]
         _lib = L
     return _lib
 
@@ -77,3 +78,14 @@ class Emu:
                           b[1].ctypes.data_as(dp), uu.ctypes.data_as(dp), N, H.ctypes.data_as(dp),
                           dv.ctypes.data_as(dp), F.ctypes.data_as(dp), fid.ctypes.data_as(dp), N)
         return H.reshape(N, N), dv.view(np.complex128), complex(F[0], F[1])
+
+    def overlap_pad(self, dx, x, dy, y, with_dH=False):
+        """<x|y> or <x|dH|y> on the padded contraction (csrc/fast_overlap.hpp)"""
+        a = [np.ascontiguousarray(v, np.int32) for v in (dx, dy)]
+        b = [np.ascontiguousarray(v, np.complex128).view(np.float64) for v in (x, y)]
+        out = np.zeros(2)
+        rc = lib().emu_overlap_pad(self.h, a[0].ctypes.data_as(ip), b[0].ctypes.data_as(dp), a[1].ctypes.data_as(ip),
+                                   b[1].ctypes.data_as(dp), int(with_dH), out.ctypes.data_as(dp))
+        if rc != 0:
+            raise RuntimeError("no padded overlap plan")
+        return complex(out[0], out[1])

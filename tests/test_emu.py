@@ -86,3 +86,20 @@ def test_emulated_padded_overlap(E, monkeypatch):
     assert np.abs(Hf - Hg).max() <= 1e-13 * m
     assert np.abs(Hf - Ho).max() <= 1e-12 * m
     assert not np.array_equal(Hf, Hg)  # the padded contraction ran (a different summation order)
+
+
+@pytest.mark.parametrize("cfg", [(5, 5, 5, 1.0, 2.5, 50.0), (4, 3, 4, 1.0, 2.0, 10.0)])
+def test_emulated_padded_overlap_pairs(E, cfg):
+    """<x|y> and <x|dH|y> on the padded contraction (k_overlaps_pad's body:
+    divT, F, fidelities on the one-wave contexts) against the oracle, also for
+    stepped states whose bond dimensions sit below the padded bounds"""
+    Lx, px, Qx, J, U1, U2 = cfg
+    d1, x1 = _gs(Lx, px, Qx, J, U1)
+    d2, x2 = _gs(Lx, px, Qx, J, U2)
+    st = O.Stepper(Lx, px, Qx, J, 0.01, 1e-4, 80)
+    e = E.Emu(Lx, px, Qx, J, 0.01, 1e-4, 80, True)
+    d3, x3 = e.steps(d1, x1, np.random.default_rng(9).uniform(2.0, 10.0, 6), True)
+    for (da, xa), (db, xb) in [((d1, x1), (d2, x2)), ((d2, x2), (d3, x3)), ((d3, x3), (d3, x3))]:
+        a, b = O.MPS(Lx, px, Qx, da, xa), O.MPS(Lx, px, Qx, db, xb)
+        assert abs(e.overlap_pad(da, xa, db, xb) - st.overlap(a, b)) <= 1e-12
+        assert abs(e.overlap_pad(da, xa, db, xb, True) - st.overlap_dH(a, b)) <= 1e-12 * max(1.0, abs(st.overlap_dH(a, b)))
