@@ -701,6 +701,14 @@ __device__ __forceinline__ T block_sum_t(T v, T* red) {
   for (int i = 0; i < TNT / 64; ++i) s += red[i];
   return s;
 }
+// Every step below is the round-5 kernel's arithmetic in the same order (so the
+// kept counts and weights are bit-identical); what changed is where latency
+// went: the problems' sizes and eigenvalue pointers are read by one thread per
+// problem at once (not one problem after another), the eigenvalues are gathered
+// by flat index, the global rank comes from binary searches in the other
+// sectors' descending lists (not an all-pairs count), the suffix rule reads its
+// sorted values eight at a time, and the kept counts stay in LDS.
+constexpr int kTruncMaxNp = 128;  // problems per item on the fast path (more: the all-pairs rank)
 __global__ __launch_bounds__(TNT) void k_truncate(const TItem* __restrict__ items, const EProb* __restrict__ probs) {
   extern __shared__ __align__(16) char smem[];
   const TItem I = items[blockIdx.x];
@@ -711,28 +719,99 @@ __global__ __launch_bounds__(TNT) void k_truncate(const TItem* __restrict__ item
   int* PO = RK + kMaxEig;            // problem offsets (np + 1)
   __shared__ double red[TNT / 64];
   __shared__ int sm[2];
-  if (tid == 0) {
+  __shared__ const double* WP[kTruncMaxNp];
+  __shared__ int KQ[kTruncMaxNp];
+  __shared__ int unsorted;
+  const int np = I.np;
+  const bool fastp = np <= kTruncMaxNp;
+  if (fastp) {
+    for (int i = tid; i < np; i += TNT) {
+      const EProb& P = probs[I.p0 + i];
+      PO[i] = P.n;
+      WP[i] = P.w;
+    }
+    if (tid == 0) unsorted = 0;
+    __syncthreads();
+    if (tid == 0) {
+      int o = 0;
+      for (int i = 0; i < np; ++i) {
+        const int n = PO[i];
+        PO[i] = o;
+        o += n;
+      }
+      PO[np] = o;
+    }
+  } else if (tid == 0) {
     int o = 0;
-    for (int i = 0; i < I.np; ++i) { PO[i] = o; o += probs[I.p0 + i].n; }
-    PO[I.np] = o;
+    for (int i = 0; i < np; ++i) { PO[i] = o; o += probs[I.p0 + i].n; }
+    PO[np] = o;
   }
   __syncthreads();
-  const int T = PO[I.np];
-  for (int i = 0; i < I.np; ++i) {
-    const EProb& P = probs[I.p0 + i];
-    for (int j = tid; j < P.n; j += TNT) LAM[PO[i] + j] = fmax(P.w[j], 0.0);
+  const int T = PO[np];
+  // the problem of flat index e: the last i with PO[i] <= e
+  auto prob_of = [&](int e) {
+    int lo = 0, hi = np - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (PO[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  if (fastp) {
+    for (int e = tid; e < T; e += TNT) {
+      const int i = prob_of(e);
+      LAM[e] = fmax(WP[i][e - PO[i]], 0.0);
+    }
+  } else {
+    for (int i = 0; i < np; ++i) {
+      const EProb& P = probs[I.p0 + i];
+      for (int j = tid; j < P.n; j += TNT) LAM[PO[i] + j] = fmax(P.w[j], 0.0);
+    }
   }
   __syncthreads();
   // global rank: (lambda desc, flat index asc); problems are in sector order
-  for (int e = tid; e < T; e += TNT) {
-    const double l = LAM[e];
-    int rk = 0;
-    for (int f = 0; f < T; ++f) {
-      const double lf = LAM[f];
-      rk += (lf > l || (lf == l && f < e)) ? 1 : 0;
+  if (fastp) {
+    // every sector's list descending? (the multisection's midpoints of a
+    // degenerate cluster could come out a rounding step out of order)
+    for (int e = tid; e + 1 < T; e += TNT)
+      if (LAM[e] < LAM[e + 1] && prob_of(e) == prob_of(e + 1)) unsorted = 1;
+    __syncthreads();
+  }
+  if (fastp && !unsorted) {
+    // rank = the index inside its own (descending) sector + per other sector
+    // the length of its prefix ahead of it: > l after it, >= l before it
+    for (int e = tid; e < T; e += TNT) {
+      const double l = LAM[e];
+      const int i = prob_of(e);
+      int rk = e - PO[i];
+      for (int i2 = 0; i2 < np; ++i2) {
+        if (i2 == i) continue;
+        const int b = PO[i2];
+        int lo = 0, hi = PO[i2 + 1] - b;
+        const bool ge = i2 < i;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const double v = LAM[b + mid];
+          if (ge ? v >= l : v > l) lo = mid + 1;
+          else hi = mid;
+        }
+        rk += lo;
+      }
+      RK[e] = rk;
+      PP[rk] = l;
     }
-    RK[e] = rk;
-    PP[rk] = l;
+  } else {
+    for (int e = tid; e < T; e += TNT) {
+      const double l = LAM[e];
+      int rk = 0;
+      for (int f = 0; f < T; ++f) {
+        const double lf = LAM[f];
+        rk += (lf > l || (lf == l && f < e)) ? 1 : 0;
+      }
+      RK[e] = rk;
+      PP[rk] = l;
+    }
   }
   double tot = 0;
   for (int e = tid; e < T; e += TNT) tot += LAM[e];
@@ -744,12 +823,26 @@ __global__ __launch_bounds__(TNT) void k_truncate(const TItem* __restrict__ item
       const double cut = I.cutoff * tot, flo = 1e-30 * tot;
       double S = 0;
       // smallest m >= 1 such that every position j >= m is discarded (the
-      // discarded set is a suffix: both tests are monotone in j)
+      // discarded set is a suffix: both tests are monotone in j); the values
+      // are read eight ahead, the sum keeps its order
       int j = T - 1;
-      for (; j >= 1; --j) {
-        const double sj = S + PP[j];
-        if (j >= I.maxm || sj < cut || PP[j] <= flo) S = sj;
-        else break;
+      bool stop = false;
+      while (j >= 1 && !stop) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = PP[j - u >= 1 ? j - u : 1];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (!stop && j >= 1) {
+            const double sj = S + v[u];
+            if (j >= I.maxm || sj < cut || v[u] <= flo) {
+              S = sj;
+              --j;
+            } else {
+              stop = true;
+            }
+          }
+        }
       }
       m = j + 1;
     } else {
@@ -761,15 +854,19 @@ __global__ __launch_bounds__(TNT) void k_truncate(const TItem* __restrict__ item
   const int m = sm[0];
   // kept per sector: its eigenvalues of global rank < m (a prefix of its
   // descending list), capped by the sector's rank bound
-  for (int i = tid; i < I.np; i += TNT) {
+  for (int i = tid; i < np; i += TNT) {
     int kq = 0;
     for (int e = PO[i]; e < PO[i + 1]; ++e) kq += RK[e] < m ? 1 : 0;
-    I.kept[i] = kq < I.bound[i] ? kq : I.bound[i];
+    const int kb = kq < I.bound[i] ? kq : I.bound[i];
+    I.kept[i] = kb;
+    if (fastp) KQ[i] = kb;
   }
   __syncthreads();
   double kw = 0;
-  for (int i = 0; i < I.np; ++i)
-    for (int j = tid; j < I.kept[i]; j += TNT) kw += LAM[PO[i] + j];
+  for (int i = 0; i < np; ++i) {
+    const int ki = fastp ? KQ[i] : I.kept[i];
+    for (int j = tid; j < ki; j += TNT) kw += LAM[PO[i] + j];
+  }
   kw = block_sum_t(kw, red);
   if (tid == 0) {
     I.keptw[0] = kw;
