@@ -587,13 +587,14 @@ static int finish_params(ocg_ctx* c) {
     const char* no = std::getenv("OCG_NO_FAST_OVL");
     const std::vector<int> ov = ocg_host::build_overlap_plan(c->P, c->md);
     const int ob = ov.empty() ? 0 : ocg_host::overlap_lds_bytes(ov, c->P);
-    if (!ov.empty() && ob <= off && !(no && no[0] && no[0] != '0')) {
+    const int obd = ov.empty() ? 0 : ocg_host::overlap_lds_bytes(ov, c->P, true);
+    if (!ov.empty() && ob <= off && obd <= 65536 && !(no && no[0] && no[0] != '0')) {
       HIPCHK(c, hipMalloc(&c->d_oplan, sizeof(int) * ov.size()));
       HIPCHK(c, hipMemcpyAsync(c->d_oplan, ov.data(), sizeof(int) * ov.size(), hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       c->P.oplan = c->d_oplan;
       c->P.ovl_bytes = ob;
-      c->P.ovl_dh_bytes = ocg_host::overlap_lds_bytes(ov, c->P, true);
+      c->P.ovl_dh_bytes = obd;
       if (std::getenv("OCG_FAST_DUMP"))
         std::fprintf(stderr, "[fast ovl] np %d nblk %d ints %d bytes %d\n", ov[ocg::fastp::kOvNp],
                      ov[ocg::fastp::kOvNblk], ov[ocg::fastp::kOvNint], ob);
