@@ -254,8 +254,8 @@ struct Engine {
                        ? std::atoi(std::getenv("OCG_HBM_THRESH"))
                        : 48;
   // register-path Gram blocks of order >= split_min leave their multisection to
-  // k_heev_bisect_split (SPE eigenvalues per workgroup on many CUs) and
-  // k_heev_bisect_fill; OCG_HBM_SPLITMIN=n moves the threshold, 0 turns it off
+  // k_heev_bisect_split (split_spe eigenvalues per workgroup on many CUs);
+  // OCG_HBM_SPLITMIN=n moves the threshold, 0 turns it off
   int split_min = std::getenv("OCG_HBM_SPLITMIN") ? std::atoi(std::getenv("OCG_HBM_SPLITMIN")) : 96;
   // eigenvalues per k_heev_bisect_split workgroup (RNT / split_spe threads each): 8, 16 or 32
   int split_spe = [] {
@@ -1037,10 +1037,11 @@ struct Engine {
         std::vector<int2> tasks;
         for (int i : split)
           for (int c = 0; split_spe * c < R.probs[i].n; ++c) tasks.push_back(make_int2(i, c));
+        // one completion counter per problem of the decomposition (k_heev_bisect_split's last-workgroup fill)
+        int* dctr = walloc<int>(size_t(np));
+        HCK(hipMemsetAsync(dctr, 0, sizeof(int) * size_t(np), st));
         hipLaunchKernelGGL(k_heev_bisect_split, dim3(int(tasks.size())), dim3(RNT), bisect_split_lds_bytes(max_split),
-                           st, R.d_probs, upload(tasks), split_spe);
-        hipLaunchKernelGGL(k_heev_bisect_fill, dim3(int(split.size())), dim3(RNT), bisect_split_lds_bytes(max_split),
-                           st, R.d_probs, upload(split));
+                           st, R.d_probs, upload(tasks), split_spe, dctr);
         HCK(hipGetLastError());
         ++split_launches;
         split_blocks += long(split.size());

@@ -820,12 +820,13 @@ __host__ __device__ constexpr int bisect_lds_bytes(int n) { return 4 * n * 8 + 4
 // one CU, 32 % of the kernel at n = 192, while the launch's other CUs have long
 // finished their smaller blocks.  Blocks of order >= the split threshold are
 // marked defer (the register kernel stops after the tridiagonal) and their
-// eigenvalues are resolved here by ceil(n / SPE) workgroups each: SPE
-// eigenvalues per workgroup, RNT / SPE = 8 threads (33 shifts) per eigenvalue,
-// 10 rounds instead of 22.  Same bounds, tolerances and unresolved threshold as
-// bisect_all (every workgroup of a block computes them identically); the
-// unresolved eigenvalues' mean needs all resolved ones, so k_heev_bisect_fill
-// sets it afterwards.
+// eigenvalues are resolved here by ceil(n / spe) workgroups each: spe
+// eigenvalues per workgroup, RNT / spe threads per eigenvalue (one shift each,
+// EProb::ks = 1: RNT / spe + 1 sub-intervals per round).  Same bounds,
+// tolerances and unresolved threshold as bisect_all (every workgroup of a block
+// computes them identically).  The unresolved eigenvalues' mean needs all the
+// resolved ones: the block's last workgroup to finish sets it (a per-block
+// counter, zeroed by the host before the launch).
 constexpr int SPE = 32;  // the largest chunk (split_spe: eigenvalues per workgroup, a divisor of RNT)
 // bounds, tolerances and the number of resolved eigenvalues of (Ld, Le2) (uniform)
 struct BisectBounds {
@@ -882,7 +883,8 @@ __device__ __forceinline__ BisectBounds bisect_bounds(const double* Ld, const do
 }
 // problem t.x, eigenvalues [SPE t.y, SPE t.y + SPE) of the resolved ones (descending)
 __global__ __launch_bounds__(RNT) void k_heev_bisect_split(const EProb* __restrict__ probs,
-                                                           const int2* __restrict__ tasks, int spe) {
+                                                           const int2* __restrict__ tasks, int spe,
+                                                           int* __restrict__ ctr) {
   extern __shared__ __align__(16) char smem_sp[];
   const int2 tk = tasks[blockIdx.x];
   const EProb P = probs[tk.x];
@@ -898,31 +900,24 @@ __global__ __launch_bounds__(RNT) void k_heev_bisect_split(const EProb* __restri
   __syncthreads();
   const BisectBounds B = bisect_bounds<RNT>(Ld, Le2, n, P.thr_rel);
   const int t0 = spe * tk.y;
-  if (t0 >= B.nres) return;  // uniform
-  const int ne = B.nres - t0 < spe ? B.nres - t0 : spe;
-  const double gl0 = B.nres < n ? fmax(B.gl, B.thr) : B.gl;
-  // RNT / spe threads per eigenvalue (also when ne < spe: the same points)
-  if (P.ks == 1) multisect<1, RNT>(Ld, Le2, n, gl0, B.gu, B.atol, B.pivmin, t0, ne, RNT / spe, P.w, lo, hi, cnt);
-  else multisect<4, RNT>(Ld, Le2, n, gl0, B.gu, B.atol, B.pivmin, t0, ne, RNT / spe, P.w, lo, hi, cnt);
-}
-__host__ __device__ constexpr int bisect_split_lds_bytes(int n) { return 16 * n + 64; }
-// the unresolved eigenvalues of a split problem: their mean (trace minus the
-// resolved ones), as bisect_all sets them; one workgroup per problem
-__global__ __launch_bounds__(RNT) void k_heev_bisect_fill(const EProb* __restrict__ probs,
-                                                          const int* __restrict__ idx) {
-  extern __shared__ __align__(16) char smem_fl[];
-  const EProb P = probs[idx[blockIdx.x]];
-  const int n = P.n, tid = threadIdx.x;
-  double* Ld = reinterpret_cast<double*>(smem_fl);
-  double* Le2 = Ld + n;
-  __shared__ double bb[RNT / 64];
-  for (int i = tid; i < n; i += RNT) {
-    Ld[i] = P.d[i];
-    Le2[i] = P.e[i] * P.e[i];
+  if (t0 < B.nres) {  // uniform
+    const int ne = B.nres - t0 < spe ? B.nres - t0 : spe;
+    const double gl0 = B.nres < n ? fmax(B.gl, B.thr) : B.gl;
+    // RNT / spe threads per eigenvalue (also when ne < spe: the same points)
+    if (P.ks == 1) multisect<1, RNT>(Ld, Le2, n, gl0, B.gu, B.atol, B.pivmin, t0, ne, RNT / spe, P.w, lo, hi, cnt);
+    else multisect<4, RNT>(Ld, Le2, n, gl0, B.gu, B.atol, B.pivmin, t0, ne, RNT / spe, P.w, lo, hi, cnt);
   }
+  if (B.nres >= n) return;  // uniform: nothing unresolved, no count
+  // every thread releases its eigenvalue stores, one lane counts; the block's
+  // last workgroup acquires them and sets the unresolved ones to their mean
+  __shared__ int last;
+  __shared__ double bb[RNT / 64];
+  __threadfence();
   __syncthreads();
-  const BisectBounds B = bisect_bounds<RNT>(Ld, Le2, n, P.thr_rel);
-  if (B.nres >= n) return;  // uniform
+  if (tid == 0) last = atomicAdd(ctr + tk.x, 1) == (n + spe - 1) / spe - 1;
+  __syncthreads();
+  if (!last) return;  // uniform
+  __threadfence();
   double sr = 0;
   for (int t = tid; t < B.nres; t += RNT) sr += P.w[t];
   for (int o = 32; o > 0; o >>= 1) sr += __shfl_xor(sr, o, 64);
@@ -933,7 +928,7 @@ __global__ __launch_bounds__(RNT) void k_heev_bisect_fill(const EProb* __restric
   const double mean = fmin(fmax((B.tr - sr) / (n - B.nres), 0.0), B.thr);
   for (int t = B.nres + tid; t < n; t += RNT) P.w[t] = mean;
 }
-
+__host__ __device__ constexpr int bisect_split_lds_bytes(int n) { return 16 * n + 64; }
 // One launch per decomposition: each workgroup picks the variant for its
 // block's order (register slot grid 2 / 4 / 8 / 12 / 13, or the LDS / L2
 // kernel for tiny and oversized blocks).  idx lists the problems, largest

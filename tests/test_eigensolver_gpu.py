@@ -137,10 +137,10 @@ def _decomp_env(monkeypatch, env, Ms, cutoff, maxm):
 
 def test_split_multisection_vs_numpy_and_in_kernel(monkeypatch):
     """register-path blocks of order >= 96 (config 4's largest sectors) leave
-    their eigenvalues to k_heev_bisect_split / k_heev_bisect_fill (32 per
-    workgroup, 8 threads each): against numpy, and against the in-kernel
+    their eigenvalues to k_heev_bisect_split (16 per
+    workgroup, 16 threads each): against numpy, and against the in-kernel
     multisection (OCG_HBM_SPLITMIN=0) to rounding, including a rank-deficient
-    block (unresolved eigenvalues below the threshold: the fill kernel's mean)
+    block (unresolved eigenvalues below the threshold: the last workgroup sets their mean)
     and a degenerate cluster; orders below the threshold stay in-kernel"""
     rng = np.random.default_rng(96)
     spec = np.exp(-np.arange(160) / 6.0)
