@@ -809,13 +809,13 @@ def bench_c4(args):
             # the sample's parts (hbm timers: kind 3 = the row batches of the two-phase path). The
             # rows of a sample run in smaller lockstep batches than the whole Hessian's (32 rows vs
             # 799 joining over the horizon), so their row-step rate is a lower bound of the whole
-            # run's; the whole getHessian is not priced from it (measured whole: 357.6 s, r06)
+            # run's; the whole getHessian is not priced from it (measured whole: 345.9 s, r06)
             rows_ms = eng.stats(3)["ms"] / args.steps
             res["horizon_sample"] = {
                 "rows": R, "of_rows": Nt - 2, "row_steps": row_steps, "of_row_steps": (Nt - 2) * (Nt - 3) // 2,
                 "precompute_ms": 1e3 * elapsed / args.steps - rows_ms, "rows_ms": rows_ms,
                 "row_steps_per_s": row_steps / max(rows_ms * 1e-3, 1e-9),
-                "whole_getHessian_measured_s": 357.6,
+                "whole_getHessian_measured_s": 345.9,
                 "whole_source": "profiles/r06_bench_c4full.json (round 6 code: one GPU, the two-phase path; "
                                 "rounds 4-5: 359-366 s, profiles/r04_bench_c4full_prio.json)"}
         res["env"] = run_env()
