@@ -336,3 +336,69 @@ def test_c4_w256_hessian_long_vs_oracle(c4, warm256, monkeypatch, pipe, path):
     assert np.abs(g - z["grad"]).max() <= 1e-6
     assert np.abs(H - z["H"]).max() <= 1e-6 * np.abs(z["H"]).max()
     eng.close()
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_horizon_local_steps_vs_oracle(c4, warm256, tmp_path):
+    """config 4 at its full horizon (N_t = 801, Maxm 256, GRAPE controls U(2,10),
+    seed 9801): the GPU engine's psi and xi trajectories (800 chi = 256 steps
+    each) checked against the oracle one step at a time at the start, middle
+    and end of the horizon — the oracle steps the GPU's own state k and its
+    result must have the GPU's bond dimensions at k +- 1 and overlap the GPU's
+    state there to 1e-9 — plus divT at three times and F, the oracle's
+    contractions of the GPU's states.  The whole-horizon oracle run (1600
+    steps and 800 dH applications at ~6 s / 19 s each on 8 cores) does not
+    fit a test or a fixture budget; these local checks pin every step they
+    sample without accumulating rounding over the horizon.  The oracle runs in
+    a CPU-only child (tests/oracle_local_steps.py) with its Householder + QL
+    eigensolver."""
+    import subprocess
+    import sys
+    from optimalcontrolmps_amd.native import Engine
+    Nt = 801
+    u = np.random.default_rng(9801).uniform(2.0, 10.0, Nt)
+    tgt = _mps(c4["w256h/tgt_dims"], c4["w256h/tgt_data"])
+    eng = Engine(L, p, N, J, DT, CUT, 256, engine="hbm")
+    eng.set_states(tgt, warm256)
+    eng.propagate(u, 3)
+    divT, F = eng.div_t(), eng.overlap_factor()
+    job = {"L": L, "p": p, "Q": N, "J": J, "dt": DT, "cutoff": CUT, "maxm": 256}
+    put = lambda key, m: job.update({key + "_dims": m.dims, key + "_data": m.data})
+    # (trajectory, from time k): psi steps k -> k + 1 forward, xi steps k -> k - 1 backward
+    steps = [(0, 0), (0, Nt // 2), (0, Nt - 2), (1, Nt - 1), (1, Nt // 2), (1, 1)]
+    nxt_bonds = []
+    for j, (w, k) in enumerate(steps):
+        k2 = k + 1 if w == 0 else k - 1
+        put(f"s{j}", eng.state(w, k))
+        nb = eng.state(w, k2)
+        put(f"n{j}", nb)
+        nxt_bonds.append(list(nb.bond_dims()))
+        job[f"u{j}"] = np.array([u[k], u[k2], 1.0 if w == 0 else 0.0])
+    job["nstep"] = len(steps)
+    dh_t = [0, Nt // 2, Nt - 1]
+    for j, k in enumerate(dh_t):
+        put(f"x{j}", eng.state(1, k))
+        put(f"y{j}", eng.state(0, k))
+    job["ndh"] = len(dh_t)
+    put("ovx", eng.state(0, Nt - 1))
+    put("ovy", tgt)
+    eng.close()
+    src, dst = tmp_path / "job.npz", tmp_path / "out.npz"
+    np.savez(src, **job)
+    env = dict(os.environ, ORC_SECTOR_THREADS=str(min(16, os.cpu_count() or 1)))
+    subprocess.run([sys.executable, os.path.join(HERE, "oracle_local_steps.py"), str(src), str(dst)],
+                   check=True, timeout=800, env=env)
+    r = np.load(dst, allow_pickle=False)
+    fid = [abs(complex(r[f"ov{j}"][0]) / np.sqrt(complex(r[f"nn{j}"][0]).real * complex(r[f"gg{j}"][0]).real) - 1.0)
+           for j in range(len(steps))]
+    print(f"full horizon: max |<oracle|gpu> - 1| {max(fid):.2e}; divT rel "
+          f"{max(abs(complex(r[f'dh{j}'][0]) - divT[k]) for j, k in enumerate(dh_t)) / np.abs(divT).max():.2e}; "
+          f"F rel {abs(complex(r['ov'][0]) - F) / abs(F):.2e}", flush=True)
+    for j in range(len(steps)):
+        assert list(r[f"bonds{j}"]) == nxt_bonds[j], (steps[j], list(r[f"bonds{j}"]), nxt_bonds[j])
+        ov, nn, gg = complex(r[f"ov{j}"][0]), complex(r[f"nn{j}"][0]), complex(r[f"gg{j}"][0])
+        assert abs(ov / np.sqrt(nn.real * gg.real) - 1.0) <= 1e-9, (steps[j], ov, nn, gg)
+    scale = np.abs(divT).max()
+    for j, k in enumerate(dh_t):
+        assert abs(complex(r[f"dh{j}"][0]) - divT[k]) <= 1e-9 * scale, (k, r[f"dh{j}"][0], divT[k])
+    assert abs(complex(r["ov"][0]) - F) <= 1e-9 * abs(F) + 1e-12
