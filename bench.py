@@ -743,14 +743,15 @@ def bench_c4(args):
     gm = eng.stats(7)   # k_gemm: the MFMA-FP64 contraction kernel
     # one bare psi chain (ocg_propagate(u, 1)) outside the timed region: the single-chain step rate
     t_sc = None
-    if not args.profiled and not (grad and c5):   # a profiled command holds only the timed population;
-        # config 5's full-horizon trajectories do not fit the device (the gradient meets in the middle)
+    paths = eng.path_stats()
+    if not args.profiled and not (grad and c5) and not paths["ckpt_runs"]:
+        # a profiled command holds only the timed population; config 5's full-horizon trajectories
+        # do not fit the device (the gradient meets in the middle, the getHessian checkpoints)
         t_sc = time.perf_counter()
         eng.propagate(control(nsteps_all), 1)
         t_sc = time.perf_counter() - t_sc
     steps_traj = 2 * (Nt - 1) * (KM if grad else 1)
     row_steps = sum(Nt - 2 - r for r in sel)   # row i steps from i to N_t-2
-    paths = eng.path_stats()
     reps = 1 if strong else world   # independent Hessians / gradients per step
     sweep = args.steps * (steps_traj * (world if (strong or grad) else reps) + (0 if grad else row_steps * reps))
     gemm_ms = gm["ms"] / max(1, gm["launches"])
